@@ -1,0 +1,237 @@
+// bsgp_fft.hpp — mixed-radix Stockham FFT core shared by the gfx950 kernels and
+// the host-side unit test (tests/cpp/fft_core_test.cpp).
+//
+// This replaces numpy's pocketfft calls on the reference hot path:
+//   restoration/sgp.py:109,113-115 (circular A/AT: fftn / ifftn of 2-D images)
+//   restoration/sgp.py:138,157 -> astropy convolve_fft (linear A/AT, zero-filled)
+//
+// Design (MI355X-first):
+//   * one 1-D transform is owned by ONE 64-lane wavefront and lives in LDS;
+//     stages ping-pong between two per-wave LDS buffers, so a stage boundary
+//     needs only a wave-level LDS sync, never a workgroup barrier;
+//   * radix 2/3/4/5 butterflies are unrolled; any other prime factor goes
+//     through a direct O(R^2) DFT stage (needed only for odd stamp sizes such
+//     as the 31x31 star stamps of application_sgp_star_stamps.py);
+//   * twiddles come from one table tw[k] = exp(-2*pi*i*k/n), k in [0,n),
+//     computed once per plan on the host in long double.
+//
+// The stage formulation is the classic Stockham autosort (decimation in time):
+//   for Ns = 1; Ns < n; Ns *= R:   out[(j/Ns)*Ns*R + j%Ns + r*Ns] =
+//        DFT_R( in[j + r*n/R] * w^(r*(j%Ns)) ),  w = exp(-2*pi*i/(Ns*R)).
+#pragma once
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define BSGP_HD __host__ __device__ __forceinline__
+#else
+#define BSGP_HD inline
+#endif
+
+namespace bsgp {
+
+struct alignas(16) cd {
+  double x, y;
+};
+
+BSGP_HD cd cmk(double x, double y) { cd r; r.x = x; r.y = y; return r; }
+BSGP_HD cd cadd(cd a, cd b) { return cmk(a.x + b.x, a.y + b.y); }
+BSGP_HD cd csub(cd a, cd b) { return cmk(a.x - b.x, a.y - b.y); }
+BSGP_HD cd cmul(cd a, cd b) { return cmk(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+// a * conj(w)
+BSGP_HD cd cmulc(cd a, cd w) { return cmk(a.x * w.x + a.y * w.y, a.y * w.x - a.x * w.y); }
+BSGP_HD cd cscale(cd a, double s) { return cmk(a.x * s, a.y * s); }
+BSGP_HD cd cconj(cd a) { return cmk(a.x, -a.y); }
+// multiply by -i (forward) or +i (inverse)
+BSGP_HD cd mul_mi(cd a, bool inv) { return inv ? cmk(-a.y, a.x) : cmk(a.y, -a.x); }
+
+constexpr int kMaxStages = 16;
+
+// One 1-D transform length with its stage radices and twiddle table.
+struct FftPlan {
+  int n;
+  int ns;
+  int radix[kMaxStages];
+  const cd* tw;  // n entries, exp(-2*pi*i*k/n)
+};
+
+BSGP_HD cd tw_at(const cd* tw, int k, bool inv) {
+  cd w = tw[k];
+  return inv ? cconj(w) : w;
+}
+
+// ---- unrolled butterflies (forward: w = exp(-2 pi i / R); inverse: conj) ----
+BSGP_HD void bfly2(cd* v) {
+  cd a = v[0], b = v[1];
+  v[0] = cadd(a, b);
+  v[1] = csub(a, b);
+}
+
+BSGP_HD void bfly3(cd* v, bool inv) {
+  const double h = 0.86602540378443864676;  // sin(2 pi / 3)
+  cd s = cadd(v[1], v[2]);
+  cd d = csub(v[1], v[2]);
+  cd t = cmk(v[0].x - 0.5 * s.x, v[0].y - 0.5 * s.y);
+  cd u = mul_mi(cscale(d, h), inv);  // -i*h*d (fwd)
+  v[0] = cadd(v[0], s);
+  v[1] = cadd(t, u);
+  v[2] = csub(t, u);
+}
+
+BSGP_HD void bfly4(cd* v, bool inv) {
+  cd s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
+  cd s13 = cadd(v[1], v[3]), d13 = mul_mi(csub(v[1], v[3]), inv);
+  v[0] = cadd(s02, s13);
+  v[2] = csub(s02, s13);
+  v[1] = cadd(d02, d13);
+  v[3] = csub(d02, d13);
+}
+
+BSGP_HD void bfly5(cd* v, bool inv) {
+  const double c1 = 0.30901699437494742410;   // cos(2 pi / 5)
+  const double c2 = -0.80901699437494742410;  // cos(4 pi / 5)
+  const double s1 = 0.95105651629515357212;   // sin(2 pi / 5)
+  const double s2 = 0.58778525229247312917;   // sin(4 pi / 5)
+  cd b1 = cadd(v[1], v[4]), b2 = cadd(v[2], v[3]);
+  cd d1 = csub(v[1], v[4]), d2 = csub(v[2], v[3]);
+  cd a0 = v[0];
+  cd t1 = cmk(a0.x + c1 * b1.x + c2 * b2.x, a0.y + c1 * b1.y + c2 * b2.y);
+  cd t2 = cmk(a0.x + c2 * b1.x + c1 * b2.x, a0.y + c2 * b1.y + c1 * b2.y);
+  cd u1 = mul_mi(cmk(s1 * d1.x + s2 * d2.x, s1 * d1.y + s2 * d2.y), inv);
+  cd u2 = mul_mi(cmk(s2 * d1.x - s1 * d2.x, s2 * d1.y - s1 * d2.y), inv);
+  v[0] = cadd(a0, cadd(b1, b2));
+  v[1] = cadd(t1, u1);
+  v[4] = csub(t1, u1);
+  v[2] = cadd(t2, u2);
+  v[3] = csub(t2, u2);
+}
+
+// One Stockham stage with a compile-time radix. `lane` in [0, nlanes).
+template <int R>
+BSGP_HD void stage_fixed(const cd* in, cd* out, int n, int Ns, const cd* tw, bool inv,
+                         int lane, int nlanes) {
+  const int nb = n / R;
+  const int twstep = n / (Ns * R);
+  for (int j = lane; j < nb; j += nlanes) {
+    const int jm = j % Ns;
+    cd v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = in[j + r * nb];
+    if (Ns > 1) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw_at(tw, r * jm * twstep, inv));
+    }
+    if constexpr (R == 2) bfly2(v);
+    if constexpr (R == 3) bfly3(v, inv);
+    if constexpr (R == 4) bfly4(v, inv);
+    if constexpr (R == 5) bfly5(v, inv);
+    const int od = (j / Ns) * Ns * R + jm;
+#pragma unroll
+    for (int r = 0; r < R; ++r) out[od + r * Ns] = v[r];
+  }
+}
+
+// Direct-DFT stage for any radix R (used for prime factors > 5).
+BSGP_HD void stage_generic(const cd* in, cd* out, int n, int R, int Ns, const cd* tw, bool inv,
+                           int lane, int nlanes) {
+  const int nb = n / R;
+  const int twstep = n / (Ns * R);
+  const int rstep = n / R;  // tw[m*rstep] = exp(-2 pi i m / R)
+  for (int j = lane; j < nb; j += nlanes) {
+    const int jm = j % Ns;
+    const int od = (j / Ns) * Ns * R + jm;
+    for (int k = 0; k < R; ++k) {
+      cd acc = cmk(0.0, 0.0);
+      for (int r = 0; r < R; ++r) {
+        cd v = in[j + r * nb];
+        if (Ns > 1 && r > 0) v = cmul(v, tw_at(tw, r * jm * twstep, inv));
+        acc = cadd(acc, cmul(v, tw_at(tw, ((r * k) % R) * rstep, inv)));
+      }
+      out[od + k * Ns] = acc;
+    }
+  }
+}
+
+BSGP_HD void fft_stage(const cd* in, cd* out, int n, int R, int Ns, const cd* tw, bool inv,
+                       int lane, int nlanes) {
+  switch (R) {
+    case 2: stage_fixed<2>(in, out, n, Ns, tw, inv, lane, nlanes); break;
+    case 3: stage_fixed<3>(in, out, n, Ns, tw, inv, lane, nlanes); break;
+    case 4: stage_fixed<4>(in, out, n, Ns, tw, inv, lane, nlanes); break;
+    case 5: stage_fixed<5>(in, out, n, Ns, tw, inv, lane, nlanes); break;
+    default: stage_generic(in, out, n, R, Ns, tw, inv, lane, nlanes); break;
+  }
+}
+
+// Run all stages of `p` on data in `a` (scratch `b`); returns the buffer that
+// holds the result (a or b). `sync()` is called after every stage.
+template <class Sync>
+BSGP_HD cd* fft_run(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlanes, Sync sync) {
+  cd* in = a;
+  cd* out = b;
+  int Ns = 1;
+  for (int s = 0; s < p.ns; ++s) {
+    const int R = p.radix[s];
+    fft_stage(in, out, p.n, R, Ns, p.tw, inv, lane, nlanes);
+    sync();
+    Ns *= R;
+    cd* t = in;
+    in = out;
+    out = t;
+  }
+  return in;
+}
+
+// ---- two real rows per complex transform -------------------------------------
+// Forward: z = a + i*b (a, b real rows of length Q) was transformed to Z.
+// Half spectra A_k = (Z_k + conj(Z_{-k}))/2, B_k = -i/2 (Z_k - conj(Z_{-k})).
+BSGP_HD void r2c_split(const cd* Z, int Q, int k, cd* A, cd* B) {
+  const cd zk = Z[k];
+  const cd zm = Z[k == 0 ? 0 : Q - k];
+  *A = cmk(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
+  // Z_k - conj(Z_m) = (p, q);  -i/2 (p + i q) = (q/2, -p/2)
+  const double p = zk.x - zm.x, q = zk.y + zm.y;
+  *B = cmk(0.5 * q, -0.5 * p);
+}
+
+// Inverse: rebuild Z_k = A_k + i B_k over the full length from the stored
+// half spectra (k < Qh); for k >= Qh use Hermitian symmetry of A and B.
+BSGP_HD cd c2r_gather(const cd* A, const cd* B, int Q, int Qh, int k) {
+  if (k < Qh) {
+    const cd a = A[k], b = B[k];
+    return cmk(a.x - b.y, a.y + b.x);
+  }
+  const cd a = A[Q - k], b = B[Q - k];
+  return cmk(a.x + b.y, b.x - a.y);
+}
+
+// Factor n into stage radices: 4s first, then 2, 3, 5, then remaining primes.
+// Returns false when n needs more than kMaxStages stages or n < 1.
+inline bool plan_radices(int n, int* radix, int* ns) {
+  if (n < 1) return false;
+  int k = 0;
+  int m = n;
+  while (m % 4 == 0) { if (k >= kMaxStages) return false; radix[k++] = 4; m /= 4; }
+  while (m % 2 == 0) { if (k >= kMaxStages) return false; radix[k++] = 2; m /= 2; }
+  while (m % 3 == 0) { if (k >= kMaxStages) return false; radix[k++] = 3; m /= 3; }
+  while (m % 5 == 0) { if (k >= kMaxStages) return false; radix[k++] = 5; m /= 5; }
+  for (int f = 7; m > 1; f += 2) {
+    while (m % f == 0) { if (k >= kMaxStages) return false; radix[k++] = f; m /= f; }
+  }
+  *ns = k;
+  return true;
+}
+
+// Smallest 5-smooth integer >= n (scipy.fft.next_fast_len semantics for
+// complex transforms, which astropy.convolve_fft uses to size its pad).
+inline int next_fast_len(int n) {
+  if (n <= 6) return n < 1 ? 1 : n;
+  for (int m = n;; ++m) {
+    int t = m;
+    while (t % 2 == 0) t /= 2;
+    while (t % 3 == 0) t /= 3;
+    while (t % 5 == 0) t /= 5;
+    if (t == 1) return m;
+  }
+}
+
+}  // namespace bsgp

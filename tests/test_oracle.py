@@ -1,0 +1,92 @@
+"""Pins the CPU oracle (oracle/sgp_oracle.py) to the reference's own outputs
+(golden vectors produced by tests/golden/make_golden.py from /root/reference).
+CPU only."""
+import numpy as np
+import pytest
+
+import sgp_oracle as orc
+from conftest import golden, ref_kwargs
+
+CIRC = ["ngc_kl27", "ngc_beta27", "ngc_beta_adapt12", "ngc_kl_proj20", "ngc_beta_proj20",
+        "ngc_kl_stop2", "ngc_kl_stop3", "ngc_kl_stop4", "ngc_kl_noscale", "ngc_beta_stop3_flux"]
+
+
+@pytest.mark.parametrize("name", CIRC)
+def test_oracle_matches_reference_ngc(name, ngc):
+    gn, psf, bkg, obj = ngc
+    fx = golden(f"ref_{name}.npz")
+    kw = ref_kwargs(fx)
+    fn = getattr(orc, str(fx["fn"]))
+    x, it, discr, _, _ = fn(gn, psf, bkg, **kw)
+    assert it == int(fx["iters"])
+    rel = np.linalg.norm(x - fx["x"]) / np.linalg.norm(fx["x"])
+    assert rel < 1e-9, rel
+    np.testing.assert_allclose(discr, fx["discr"], rtol=1e-9)
+
+
+def test_oracle_ngc_kl27_relerr(ngc):
+    """simulation_test_sgp.py:17-34 known answer: rel. error 0.137887788241."""
+    gn, psf, bkg, obj = ngc
+    x, it, discr, _, _ = orc.sgp(gn, psf, bkg, init_recon=3, stop_criterion=1, MAXIT=27)
+    rel = np.sqrt(np.sum((x - obj) ** 2) / np.sum(obj * obj))
+    assert abs(rel - 0.137887788241) < 1e-11
+    assert len(discr) == 28 and abs(discr[0] - 40.825519776418) < 1e-9
+
+
+def test_oracle_stamp31_odd_fftshift():
+    fx = golden("ref_stamp31_beta_adapt.npz")
+    x, it, discr, _, _ = orc.sgp_betaDiv(fx["gn"], fx["psf"], np.float64(20.0), init_recon=2,
+                                         stop_criterion=1, MAXIT=15, alpha=10.0, betaParam=1.01,
+                                         adapt_beta=True)
+    assert it == int(fx["iters"])
+    np.testing.assert_allclose(x, fx["x"], rtol=1e-9, atol=1e-9 * np.abs(fx["x"]).max())
+
+
+def test_oracle_projectdf_kats():
+    fx = golden("ref_projectdf_kats.npz")
+    for i in range(int(fx["ncases"])):
+        b, scaling, sat, lam0, dl0, maxp = fx[f"meta{i}"]
+        x = orc.projectDF(np.float64(b), fx[f"c{i}"], fx[f"dia{i}"], scaling,
+                          ccd_sat_level=None if np.isnan(sat) else sat, lambda_=lam0,
+                          dlambda_=dl0, max_projs=int(maxp))
+        np.testing.assert_array_equal(x, fx[f"x{i}"])
+    # every reference line incl. the overflow break (:72), ru/rl returns (:84-93), quirk (:122)
+    assert {72, 85, 90, 122}.issubset(set(fx["lines_hit"].tolist()))
+
+
+def test_oracle_betadiv_kats():
+    fx = golden("ref_betadiv_kats.npz")
+    for i, b in enumerate(fx["betas"]):
+        assert np.isclose(orc.betaDiv(fx["y"], fx["x"], b), fx[f"div{i}"], rtol=1e-13, atol=0)
+        d = orc.betaDivDeriv(fx["y"], fx["x"], b)
+        np.testing.assert_allclose(np.broadcast_to(d, fx["y"].shape), fx[f"deriv{i}"], rtol=1e-12)
+    assert abs(float(fx["kat_deriv_sum"]) - 24.66966641215759) < 1e-12
+    TF = np.fft.fftn(np.fft.fftshift(fx["wrtY_psf"]))
+    AT = lambda v: np.real(np.fft.ifftn(np.conj(TF) * np.fft.fftn(np.reshape(v, (16, 16))))).flatten()
+    for i, b in enumerate(fx["wrtY_betas"]):
+        g = orc.betaDivDerivwrtY(AT, fx["wrtY_den"], fx["wrtY_img"].flatten(), b)
+        np.testing.assert_allclose(g, fx[f"wrtY{i}"], rtol=1e-12, atol=1e-14)
+
+
+def test_oracle_linear_conv_matches_astropy():
+    fx = golden("ref_linear_conv.npz")
+    for i in range(int(fx["n"])):
+        x, k = fx[f"x{i}"], fx[f"k{i}"]
+        np.testing.assert_allclose(orc.convolve_fft_fill(x, k), fx[f"A{i}"], rtol=1e-12, atol=1e-13)
+        np.testing.assert_allclose(orc.convolve_fft_fill(x, k.conj().T), fx[f"AT{i}"], rtol=1e-12,
+                                   atol=1e-13)
+
+
+@pytest.mark.parametrize("name", ["lin64_kl", "lin64_beta", "lin256_beta", "lin256_kl",
+                                  "lin64_beta_bmap"])
+def test_oracle_linear_solves(name):
+    fx = golden(f"ref_{name}.npz")
+    kw = ref_kwargs(fx)
+    if not np.isnan(fx["flux"]):
+        kw["flux"] = np.float64(fx["flux"])
+    bkg = fx["bkg"] if fx["bkg"].ndim else np.float64(fx["bkg"])
+    x, it, discr, _, _ = getattr(orc, str(fx["fn"]))(fx["gn"].astype(np.float64), fx["psf"], bkg, **kw)
+    assert it == int(fx["iters"])
+    rel = np.linalg.norm(x - fx["x"]) / np.linalg.norm(fx["x"])
+    assert rel < 1e-8, rel
+    np.testing.assert_allclose(discr, fx["discr"], rtol=1e-8)
