@@ -1,0 +1,263 @@
+"""ctypes binding of libbsgp.so (include/bsgp.h) — the only way the Python
+drop-in reaches the GPU.  There is no CPU fallback: if the library or a
+device is missing, every entry point raises ``BsgpError``.
+
+PyTorch is imported *before* the library is loaded so that the process holds
+exactly one HIP runtime (torch ships its own ``libamdhip64.so``; the library's
+``libamdhip64.so.7`` dependency then binds to it).  Torch is used for device
+memory and the current stream only; no torch type crosses the C ABI.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+try:  # one HIP runtime per process: torch's, loaded first
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover - torch is part of the image
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("BSGP_LIB", os.path.join(_HERE, "libbsgp.so"))
+
+BSGP_CONV_CIRCULAR = 0
+BSGP_CONV_LINEAR_FILL = 1
+BSGP_VARIANT_KL = 0
+BSGP_VARIANT_BETA = 1
+BSGP_ERR_PSF = -4
+
+
+class BsgpError(RuntimeError):
+    """A failure reported by libbsgp (status code + bsgp_last_error())."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"libbsgp error {code}: {msg}")
+        self.code = code
+
+
+class Params(ctypes.Structure):
+    _fields_ = [
+        ("variant", ctypes.c_int32), ("init_recon", ctypes.c_int32),
+        ("proj_type", ctypes.c_int32), ("stop_criterion", ctypes.c_int32),
+        ("MAXIT", ctypes.c_int32), ("M_alpha", ctypes.c_int32), ("M", ctypes.c_int32),
+        ("max_projs", ctypes.c_int32),
+        ("gamma", ctypes.c_double), ("beta", ctypes.c_double), ("alpha", ctypes.c_double),
+        ("alpha_min", ctypes.c_double), ("alpha_max", ctypes.c_double), ("tau", ctypes.c_double),
+        ("ccd_sat_level", ctypes.c_double), ("betaParam", ctypes.c_double),
+        ("lr", ctypes.c_double), ("lr_exp_param", ctypes.c_double),
+        ("tol_convergence", ctypes.c_double), ("prescaled_scaling", ctypes.c_double),
+        ("prescaled_tol4", ctypes.c_double),
+        ("has_sat", ctypes.c_int32), ("scale_data", ctypes.c_int32), ("verbose", ctypes.c_int32),
+        ("adapt_beta", ctypes.c_int32), ("schedule_lr", ctypes.c_int32),
+        ("bkg_is_map", ctypes.c_int32), ("ls_spec", ctypes.c_int32), ("reserved", ctypes.c_int32),
+    ]
+
+
+_P = ctypes.c_void_p
+
+
+class Inputs(ctypes.Structure):
+    _fields_ = [("gn", _P), ("bkg", _P), ("flux", _P), ("x0", _P), ("beta0", _P)]
+
+
+class Outputs(ctypes.Structure):
+    _fields_ = [("x", _P), ("iters", _P), ("discr", _P), ("times", _P), ("crit", _P),
+                ("flags", _P), ("beta_final", _P), ("counters", _P)]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def lib():
+    """Load libbsgp.so once; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise BsgpError(-3, f"{LIB_PATH} not built — run __graft_entry__.build()")
+            L = ctypes.CDLL(LIB_PATH)
+            i32, i64, dbl, vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
+            L.bsgp_last_error.restype = ctypes.c_char_p
+            L.bsgp_abi_version.restype = i32
+            L.bsgp_plan_create.argtypes = [i32, i32, vp, i32, i32, i32, i32,
+                                           ctypes.POINTER(vp)]
+            L.bsgp_plan_destroy.argtypes = [vp]
+            L.bsgp_plan_info.argtypes = [vp, vp, vp, vp, vp]
+            L.bsgp_solve_device.argtypes = [vp, i32, vp, vp, vp, vp]
+            L.bsgp_solve_host.argtypes = [vp, i32, vp, vp, vp]
+            L.bsgp_apply_operator.argtypes = [vp, i32, i32, vp, vp, vp]
+            L.bsgp_project_df.argtypes = [i64, dbl, vp, vp, dbl, i32, dbl, dbl, dbl, dbl, i32,
+                                          i32, i32, vp, vp, vp]
+            L.bsgp_beta_div.argtypes = [i64, vp, vp, dbl, vp, vp]
+            L.bsgp_beta_div_deriv.argtypes = [i64, vp, vp, dbl, vp, vp]
+            L.bsgp_beta_div_grad_parts.argtypes = [i64, vp, vp, dbl, vp, vp, vp]
+            for name in ["bsgp_plan_create", "bsgp_plan_destroy", "bsgp_plan_info",
+                         "bsgp_solve_device", "bsgp_solve_host", "bsgp_apply_operator",
+                         "bsgp_project_df", "bsgp_beta_div", "bsgp_beta_div_deriv",
+                         "bsgp_beta_div_grad_parts", "bsgp_device_synchronize"]:
+                getattr(L, name).restype = ctypes.c_int
+            _lib = L
+    return _lib
+
+
+EXPORTED = ["bsgp_plan_create", "bsgp_plan_destroy", "bsgp_plan_info", "bsgp_solve_device",
+            "bsgp_solve_host", "bsgp_apply_operator", "bsgp_project_df", "bsgp_beta_div",
+            "bsgp_beta_div_deriv", "bsgp_beta_div_grad_parts", "bsgp_device_synchronize",
+            "bsgp_last_error", "bsgp_abi_version"]
+
+
+def check(rc):
+    if rc != 0:
+        raise BsgpError(rc, lib().bsgp_last_error().decode(errors="replace"))
+
+
+def require_gpu():
+    """The product path runs on the device or not at all."""
+    if torch is None or not torch.cuda.is_available():
+        raise BsgpError(-2, "no HIP device visible: the beta-SGP engine has no CPU fallback")
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def current_stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class Plan:
+    """A device plan: FFT geometry + PSF transfer functions (bsgp_plan_create)."""
+
+    def __init__(self, H, W, psf, conv_mode, device=None):
+        require_gpu()
+        if device is None:
+            device = torch.cuda.current_device()
+        psf = np.ascontiguousarray(psf, dtype="<f8")
+        self.H, self.W = int(H), int(W)
+        self.kh, self.kw = psf.shape
+        self.conv_mode = conv_mode
+        self.device = device
+        h = ctypes.c_void_p()
+        rc = lib().bsgp_plan_create(self.H, self.W, psf.ctypes.data, self.kh, self.kw, conv_mode,
+                                    device, ctypes.byref(h))
+        if rc != 0:
+            raise BsgpError(rc, lib().bsgp_last_error().decode(errors="replace"))
+        self.h = h
+        P, Q, wave = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        sb = ctypes.c_int64()
+        check(lib().bsgp_plan_info(h, ctypes.byref(P), ctypes.byref(Q), ctypes.byref(sb),
+                                   ctypes.byref(wave)))
+        self.P, self.Q, self.slot_bytes, self.fft_waves = P.value, Q.value, sb.value, wave.value
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and _lib is not None:
+            try:
+                _lib.bsgp_plan_destroy(h)
+            except Exception:  # pragma: no cover
+                pass
+            self.h = None
+
+    # -------------------------------------------------------------- operators
+    def apply(self, x, transpose=False):
+        """A(x) / AT(x) on a [B,H,W] (or [H,W]) float64 CUDA tensor."""
+        x = x.contiguous()
+        out = torch.empty_like(x)
+        B = 1 if x.dim() == 2 else x.shape[0]
+        check(lib().bsgp_apply_operator(self.h, B, int(transpose), _ptr(x), _ptr(out),
+                                        current_stream()))
+        return out
+
+    # ------------------------------------------------------------------ solve
+    def solve(self, gn, bkg, params, flux=None, x0=None, beta0=None, want_times=True):
+        """Batched solve on device tensors: gn [B,H,W] f64; bkg [B] or [B,H,W];
+        flux/beta0 [B] or None; x0 [B,H,W] or None.  Asynchronous on the
+        current stream; returns a dict of device output tensors."""
+        B = gn.shape[0]
+        M1 = params.MAXIT + 1
+        dev = gn.device
+        f64 = dict(dtype=torch.float64, device=dev)
+        out = {
+            "x": torch.empty_like(gn),
+            "iters": torch.zeros(B, dtype=torch.int32, device=dev),
+            "discr": torch.zeros(B, M1, **f64),
+            "times": torch.zeros(B, M1, **f64) if want_times else None,
+            "crit": torch.zeros(B, M1, **f64),
+            "flags": torch.zeros(B, M1, dtype=torch.int32, device=dev),
+            "beta_final": torch.zeros(B, **f64),
+            "counters": torch.zeros(B, 4, dtype=torch.int64, device=dev),
+        }
+        ins = Inputs(_ptr(gn), _ptr(bkg), _ptr(flux), _ptr(x0), _ptr(beta0))
+        outs = Outputs(*[_ptr(out[k]) for k in ["x", "iters", "discr", "times", "crit", "flags",
+                                                 "beta_final", "counters"]])
+        self._keep = (gn, bkg, flux, x0, beta0)
+        check(lib().bsgp_solve_device(self.h, B, ctypes.byref(params), ctypes.byref(ins),
+                                      ctypes.byref(outs), current_stream()))
+        return out
+
+
+_plan_cache = {}
+_plan_cache_lock = threading.Lock()
+
+
+def get_plan(H, W, psf, conv_mode):
+    """Plans are cached per (shape, psf bytes, mode, device)."""
+    require_gpu()
+    psf = np.ascontiguousarray(psf, dtype="<f8")
+    dev = torch.cuda.current_device()
+    key = (H, W, psf.shape, psf.tobytes(), conv_mode, dev)
+    with _plan_cache_lock:
+        p = _plan_cache.get(key)
+        if p is None:
+            if len(_plan_cache) > 16:
+                _plan_cache.clear()
+            p = Plan(H, W, psf, conv_mode, dev)
+            _plan_cache[key] = p
+    return p
+
+
+def to_dev(a):
+    a = np.ascontiguousarray(a, dtype="<f8")
+    if not a.flags.writeable:
+        a = a.copy()
+    return torch.from_numpy(a).to("cuda")
+
+
+def project_df_dev(b, c, dia, scaling, ccd_sat_level, lambda_, dlambda_, tol_lam, biter, siter,
+                   max_projs):
+    """flux_conserve_proj.projectDF on device tensors; returns (x, info[4])."""
+    x = torch.empty_like(c)
+    info = torch.zeros(4, dtype=torch.float64, device=c.device)
+    has_sat = ccd_sat_level is not None
+    check(lib().bsgp_project_df(c.numel(), float(b), _ptr(c), _ptr(dia), float(scaling),
+                                int(has_sat), float(ccd_sat_level) if has_sat else 0.0,
+                                float(lambda_), float(dlambda_), float(tol_lam), int(biter),
+                                int(siter), int(max_projs), _ptr(x), _ptr(info),
+                                current_stream()))
+    return x, info
+
+
+def beta_div_dev(y, x, beta):
+    out = torch.zeros(1, dtype=torch.float64, device=y.device)
+    check(lib().bsgp_beta_div(y.numel(), _ptr(y), _ptr(x), float(beta), _ptr(out),
+                              current_stream()))
+    return out
+
+
+def beta_div_deriv_dev(y, x, beta):
+    out = torch.empty_like(y)
+    check(lib().bsgp_beta_div_deriv(y.numel(), _ptr(y), _ptr(x), float(beta), _ptr(out),
+                                    current_stream()))
+    return out
+
+
+def grad_parts_dev(den, gn, beta):
+    p1 = torch.empty_like(den)
+    w = torch.empty_like(den)
+    check(lib().bsgp_beta_div_grad_parts(den.numel(), _ptr(den), _ptr(gn), float(beta), _ptr(p1),
+                                         _ptr(w), current_stream()))
+    return p1, w

@@ -1,0 +1,447 @@
+// bsgp_api.hip — C-ABI host layer of libbsgp.so (declared in include/bsgp.h).
+//
+// Owns plans (FFT geometry, twiddles, PSF transfer functions built on the
+// device) and per-plan workspaces; validates arguments; launches the kernels
+// of bsgp_solver.hip.  No PyTorch types cross this boundary.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "bsgp_internal.hpp"
+
+using namespace bsgp;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(BSGP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));    \
+  } while (0)
+
+size_t round_up(size_t v, size_t m) { return (v + m - 1) / m * m; }
+
+std::vector<cd> twiddles(int n) {
+  std::vector<cd> t(n);
+  const long double pi = 3.141592653589793238462643383279502884L;
+  for (int k = 0; k < n; ++k) {
+    const long double a = -2.0L * pi * (long double)k / (long double)n;
+    t[k] = cmk((double)cosl(a), (double)sinl(a));
+  }
+  return t;
+}
+
+}  // namespace
+
+struct bsgp_plan_s {
+  int device = 0;
+  int conv_mode = 0;
+  Geo g{};
+  cd* tw = nullptr;     // twiddles for P then Q
+  cd* tf = nullptr;     // tfA then tfAT, each Qh*P
+  size_t lds_fft_bytes = 0;
+  size_t lds_bytes = 0;
+  int wg_per_cu = 1;
+  int ncu = 256;
+  // solver workspace
+  double* ws = nullptr;
+  size_t ws_slots = 0;
+  size_t slot_stride = 0;
+  size_t vec_stride = 0;
+  int* queue = nullptr;
+  // operator workspace
+  cd* opws = nullptr;
+  size_t opws_slots = 0;
+};
+
+static int ensure_ws(bsgp_plan p, size_t slots) {
+  if (slots <= p->ws_slots) return BSGP_OK;
+  if (p->ws) HIP_TRY(hipFree(p->ws));
+  p->ws = nullptr;
+  p->ws_slots = 0;
+  HIP_TRY(hipMalloc(&p->ws, slots * p->slot_stride * sizeof(double)));
+  p->ws_slots = slots;
+  return BSGP_OK;
+}
+
+extern "C" {
+
+int32_t bsgp_abi_version(void) { return 1; }
+
+const char* bsgp_last_error(void) { return g_err.c_str(); }
+
+int bsgp_device_synchronize(void) {
+  HIP_TRY(hipDeviceSynchronize());
+  return BSGP_OK;
+}
+
+int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_t kw,
+                     int32_t conv_mode, int32_t device, bsgp_plan* out) {
+  if (!out) return fail(BSGP_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  if (H < 1 || W < 1 || kh < 1 || kw < 1 || !psf) return fail(BSGP_ERR_ARG, "bad shape or psf");
+  if (conv_mode != BSGP_CONV_CIRCULAR && conv_mode != BSGP_CONV_LINEAR_FILL)
+    return fail(BSGP_ERR_ARG, "bad conv_mode");
+  if (conv_mode == BSGP_CONV_CIRCULAR && (kh != H || kw != W))
+    return fail(BSGP_ERR_ARG,
+                "circular A (use_original_SGP_Afunction=True) needs psf.shape == gn.shape");
+  // PSF normalisation check (sgp.py:97-102)
+  {
+    double s = 0;
+    for (int i = 0; i < kh * kw; ++i) s += psf[i];
+    if (std::fabs(s - 1.0) > 1e4 * 2.220446049250313e-16) {
+      char b[160];
+      snprintf(b, sizeof b, "PSF is not normalized! sum(psf) - 1. = %.17g", s - 1.0);
+      return fail(BSGP_ERR_PSF, b);
+    }
+  }
+  HIP_TRY(hipSetDevice(device));
+  bsgp_plan p = new bsgp_plan_s();
+  p->device = device;
+  p->conv_mode = conv_mode;
+  Geo& g = p->g;
+  g.H = H;
+  g.W = W;
+  if (conv_mode == BSGP_CONV_CIRCULAR) {
+    g.P = H;
+    g.Q = W;
+  } else {
+    // zero-fill linear convolution on a P x Q circular grid without
+    // wrap-around for either kernel (A: kh x kw, AT: kw x kh)
+    const int km = kh > kw ? kh : kw;
+    int pmin = H + km / 2, qmin = W + km / 2;
+    if (pmin < km) pmin = km;
+    if (qmin < km) qmin = km;
+    g.P = next_fast_len(pmin);
+    g.Q = next_fast_len(qmin);
+  }
+  g.Qh = g.Q / 2 + 1;
+  g.fp.n = g.P;
+  g.fq.n = g.Q;
+  if (!plan_radices(g.P, g.fp.radix, &g.fp.ns) || !plan_radices(g.Q, g.fq.radix, &g.fq.ns)) {
+    delete p;
+    return fail(BSGP_ERR_UNSUPPORTED, "FFT length has too many factors");
+  }
+  int maxlen = g.P > g.Q ? g.P : g.Q;
+  g.lpad = maxlen + 1;
+  // LDS: nfw waves x 2 buffers, + reduction scratch + queue slot
+  const size_t red_bytes = (size_t)kWaves * kMaxRed * sizeof(double) + 16;
+  int nfw = kWaves;
+  size_t budget = 80 * 1024;  // two workgroups per CU
+  p->wg_per_cu = 2;
+  auto need = [&](int n) { return (size_t)n * 2 * g.lpad * sizeof(cd) + red_bytes; };
+  while (nfw > 1 && need(nfw) > budget) nfw--;
+  if (need(nfw) > budget) {
+    budget = 160 * 1024 - 256;
+    p->wg_per_cu = 1;
+    nfw = kWaves;
+    while (nfw > 1 && need(nfw) > budget) nfw--;
+    if (need(nfw) > budget) {
+      delete p;
+      return fail(BSGP_ERR_UNSUPPORTED, "FFT length too large for one workgroup's LDS");
+    }
+  }
+  g.nfw = nfw;
+  p->lds_fft_bytes = (size_t)nfw * 2 * g.lpad * sizeof(cd);
+  p->lds_bytes = p->lds_fft_bytes + red_bytes;
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        ncu > 0)
+      p->ncu = ncu;
+  }
+  if (set_solver_lds_limit(p->lds_bytes) != hipSuccess) {
+    delete p;
+    return fail(BSGP_ERR_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+  }
+  // twiddles
+  {
+    std::vector<cd> tw = twiddles(g.P);
+    std::vector<cd> twq = twiddles(g.Q);
+    tw.insert(tw.end(), twq.begin(), twq.end());
+    if (hipMalloc(&p->tw, tw.size() * sizeof(cd)) != hipSuccess ||
+        hipMemcpy(p->tw, tw.data(), tw.size() * sizeof(cd), hipMemcpyHostToDevice) != hipSuccess) {
+      bsgp_plan_destroy(p);
+      return fail(BSGP_ERR_HIP, "twiddle upload failed");
+    }
+    g.fp.tw = p->tw;
+    g.fq.tw = p->tw + g.P;
+  }
+  // circularly-placed kernels for A and AT on the P x Q grid
+  const size_t PQ = (size_t)g.P * g.Q;
+  std::vector<double> kA(PQ, 0.0), kAT(PQ, 0.0);
+  if (conv_mode == BSGP_CONV_CIRCULAR) {
+    // fftshift(psf): out[i][j] = psf[(i - H//2) mod H][(j - W//2) mod W]  (sgp.py:109)
+    for (int i = 0; i < H; ++i)
+      for (int j = 0; j < W; ++j) {
+        const int si = ((i - H / 2) % H + H) % H, sj = ((j - W / 2) % W + W) % W;
+        kA[(size_t)i * W + j] = psf[(size_t)si * W + sj];
+      }
+  } else {
+    // astropy convolve_fft(normalize_kernel=True): kernel/sum, centre at k//2
+    // (convolve.py:664-672, 770-787); AT uses psf.conj().T (sgp.py:157)
+    double s = 0;
+    for (int i = 0; i < kh * kw; ++i) s += psf[i];
+    for (int u = 0; u < kh; ++u)
+      for (int v = 0; v < kw; ++v) {
+        const double val = psf[(size_t)u * kw + v] / s;
+        const int a = ((u - kh / 2) % g.P + g.P) % g.P, b = ((v - kw / 2) % g.Q + g.Q) % g.Q;
+        kA[(size_t)a * g.Q + b] += val;
+        // transposed kernel T[v][u] (shape kw x kh), centre (kw//2, kh//2)
+        const int at = ((v - kw / 2) % g.P + g.P) % g.P, bt = ((u - kh / 2) % g.Q + g.Q) % g.Q;
+        kAT[(size_t)at * g.Q + bt] += val;
+      }
+  }
+  double* kc = nullptr;
+  cd* spec = nullptr;
+  const size_t tfn = (size_t)g.Qh * g.P;
+  int rc = BSGP_OK;
+  if (hipMalloc(&p->tf, 2 * tfn * sizeof(cd)) != hipSuccess ||
+      hipMalloc(&kc, 2 * PQ * sizeof(double)) != hipSuccess ||
+      hipMalloc(&spec, (size_t)g.P * g.Qh * sizeof(cd)) != hipSuccess) {
+    rc = fail(BSGP_ERR_HIP, "plan allocation failed");
+  }
+  if (rc == BSGP_OK) {
+    g.tfA = p->tf;
+    g.tfAT = p->tf + tfn;
+    const double scale = 1.0 / ((double)g.P * (double)g.Q);
+    if (hipMemcpy(kc, kA.data(), PQ * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(kc + PQ, kAT.data(), PQ * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+      rc = fail(BSGP_ERR_HIP, "psf upload failed");
+    if (rc == BSGP_OK) {
+      if (launch_build_tf(g, kc, spec, p->tf, scale, 0, p->lds_bytes, 0) != hipSuccess)
+        rc = fail(BSGP_ERR_HIP, "build_tf(A) launch failed");
+      else if (hipDeviceSynchronize() != hipSuccess)
+        rc = fail(BSGP_ERR_HIP, "build_tf(A) failed");
+    }
+    if (rc == BSGP_OK) {
+      // circular: TF_AT = conj(TF_A) (sgp.py:110); linear: FFT of the transposed kernel
+      const bool circ = conv_mode == BSGP_CONV_CIRCULAR;
+      if (launch_build_tf(g, circ ? kc : kc + PQ, spec, p->tf + tfn, scale, circ ? 1 : 0,
+                          p->lds_bytes, 0) != hipSuccess)
+        rc = fail(BSGP_ERR_HIP, "build_tf(AT) launch failed");
+      else if (hipDeviceSynchronize() != hipSuccess)
+        rc = fail(BSGP_ERR_HIP, "build_tf(AT) failed");
+    }
+  }
+  if (kc) (void)hipFree(kc);
+  if (spec) (void)hipFree(spec);
+  if (rc != BSGP_OK) {
+    std::string m = g_err;
+    bsgp_plan_destroy(p);
+    return fail(rc, m);
+  }
+  const size_t N = (size_t)H * W;
+  p->vec_stride = round_up(N, 32);
+  p->slot_stride = 8 * p->vec_stride + round_up((size_t)H * g.Qh * 2, 32);
+  if (hipMalloc(&p->queue, 256) != hipSuccess) {
+    bsgp_plan_destroy(p);
+    return fail(BSGP_ERR_HIP, "queue allocation failed");
+  }
+  *out = p;
+  return BSGP_OK;
+}
+
+int bsgp_plan_destroy(bsgp_plan p) {
+  if (!p) return BSGP_OK;
+  (void)hipSetDevice(p->device);
+  if (p->tw) (void)hipFree(p->tw);
+  if (p->tf) (void)hipFree(p->tf);
+  if (p->ws) (void)hipFree(p->ws);
+  if (p->queue) (void)hipFree(p->queue);
+  if (p->opws) (void)hipFree(p->opws);
+  delete p;
+  return BSGP_OK;
+}
+
+int bsgp_plan_info(bsgp_plan p, int32_t* P, int32_t* Q, int64_t* slot_bytes,
+                   int32_t* fft_waves) {
+  if (!p) return fail(BSGP_ERR_ARG, "plan is NULL");
+  if (P) *P = p->g.P;
+  if (Q) *Q = p->g.Q;
+  if (slot_bytes) *slot_bytes = (int64_t)(p->slot_stride * sizeof(double));
+  if (fft_waves) *fft_waves = p->g.nfw;
+  return BSGP_OK;
+}
+
+static int check_params(const bsgp_params* q) {
+  if (!q) return fail(BSGP_ERR_ARG, "params is NULL");
+  if (q->variant != BSGP_VARIANT_KL && q->variant != BSGP_VARIANT_BETA)
+    return fail(BSGP_ERR_ARG, "bad variant");
+  if (q->MAXIT < 1) return fail(BSGP_ERR_ARG, "MAXIT must be >= 1");
+  if (q->M_alpha < 1 || q->M_alpha > 32) return fail(BSGP_ERR_ARG, "M_alpha must be in [1, 32]");
+  if (q->M < 1 || q->M > 32) return fail(BSGP_ERR_ARG, "M must be in [1, 32]");
+  if (q->ls_spec < 1 || q->ls_spec > 8) return fail(BSGP_ERR_ARG, "ls_spec must be in [1, 8]");
+  if (q->init_recon < 0 || q->init_recon > 3) return fail(BSGP_ERR_ARG, "bad init_recon");
+  if (q->proj_type != 0 && q->proj_type != 1) return fail(BSGP_ERR_ARG, "bad proj_type");
+  if (q->scale_data < 0 || q->scale_data > 2) return fail(BSGP_ERR_ARG, "bad scale_data");
+  return BSGP_OK;
+}
+
+int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_inputs* in,
+                      const bsgp_outputs* out, void* stream) {
+  if (!p) return fail(BSGP_ERR_ARG, "plan is NULL");
+  int rc = check_params(prm);
+  if (rc) return rc;
+  if (B < 1) return fail(BSGP_ERR_ARG, "B must be >= 1");
+  if (!in || !in->gn || !in->bkg) return fail(BSGP_ERR_ARG, "inputs gn/bkg missing");
+  if ((prm->init_recon == 1 || prm->scale_data == 2) && !in->x0)
+    return fail(BSGP_ERR_ARG, "init_recon=1 and scale_data=2 need x0");
+  if (!out || !out->x || !out->iters || !out->discr) return fail(BSGP_ERR_ARG, "outputs missing");
+  HIP_TRY(hipSetDevice(p->device));
+  const int grid = B < p->ncu * p->wg_per_cu ? B : p->ncu * p->wg_per_cu;
+  rc = ensure_ws(p, (size_t)grid);
+  if (rc) return rc;
+  SolveArgs a;
+  a.g = p->g;
+  a.prm = *prm;
+  a.in = *in;
+  a.out = *out;
+  a.B = B;
+  a.queue = p->queue;
+  a.ws = p->ws;
+  a.slot_stride = p->slot_stride;
+  a.vec_stride = p->vec_stride;
+  a.lds_fft_bytes = p->lds_fft_bytes;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemsetAsync(p->queue, 0, 16, s));
+  HIP_TRY(launch_solve(a, grid, p->lds_bytes, s));
+  return BSGP_OK;
+}
+
+int bsgp_solve_host(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_inputs* in,
+                    const bsgp_outputs* out) {
+  if (!p) return fail(BSGP_ERR_ARG, "plan is NULL");
+  int rc = check_params(prm);
+  if (rc) return rc;
+  if (B < 1 || !in || !in->gn || !in->bkg || !out || !out->x || !out->iters || !out->discr)
+    return fail(BSGP_ERR_ARG, "bad arguments");
+  HIP_TRY(hipSetDevice(p->device));
+  const size_t N = (size_t)p->g.H * p->g.W, M1 = (size_t)prm->MAXIT + 1;
+  std::vector<void*> bufs;
+  auto dalloc = [&](size_t bytes) -> void* {
+    void* d = nullptr;
+    if (hipMalloc(&d, bytes ? bytes : 8) != hipSuccess) return nullptr;
+    bufs.push_back(d);
+    return d;
+  };
+  auto cleanup = [&]() {
+    for (void* b : bufs) (void)hipFree(b);
+  };
+  bsgp_inputs di{};
+  bsgp_outputs dout{};
+  const size_t nb = prm->bkg_is_map ? B * N : (size_t)B;
+  di.gn = (const double*)dalloc(B * N * 8);
+  di.bkg = (const double*)dalloc(nb * 8);
+  if (in->flux) di.flux = (const double*)dalloc(B * 8);
+  if (in->x0) di.x0 = (const double*)dalloc(B * N * 8);
+  if (in->beta0) di.beta0 = (const double*)dalloc(B * 8);
+  dout.x = (double*)dalloc(B * N * 8);
+  dout.iters = (int32_t*)dalloc(B * 4);
+  dout.discr = (double*)dalloc(B * M1 * 8);
+  if (out->times) dout.times = (double*)dalloc(B * M1 * 8);
+  if (out->crit) dout.crit = (double*)dalloc(B * M1 * 8);
+  if (out->flags) dout.flags = (int32_t*)dalloc(B * M1 * 4);
+  if (out->beta_final) dout.beta_final = (double*)dalloc(B * 8);
+  if (out->counters) dout.counters = (int64_t*)dalloc(B * 4 * 8);
+  for (void* b : bufs)
+    if (!b) {
+      cleanup();
+      return fail(BSGP_ERR_HIP, "device allocation failed");
+    }
+  auto h2d = [&](const void* d, const void* h, size_t bytes) {
+    return hipMemcpy(const_cast<void*>(d), h, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  };
+  bool ok = h2d(di.gn, in->gn, B * N * 8) && h2d(di.bkg, in->bkg, nb * 8) &&
+            (!in->flux || h2d(di.flux, in->flux, B * 8)) &&
+            (!in->x0 || h2d(di.x0, in->x0, B * N * 8)) &&
+            (!in->beta0 || h2d(di.beta0, in->beta0, B * 8));
+  if (!ok) {
+    cleanup();
+    return fail(BSGP_ERR_HIP, "host to device copy failed");
+  }
+  rc = bsgp_solve_device(p, B, prm, &di, &dout, nullptr);
+  if (rc) {
+    std::string m = g_err;
+    cleanup();
+    return fail(rc, m);
+  }
+  auto d2h = [&](void* h, const void* d, size_t bytes) {
+    return !h || hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost) == hipSuccess;
+  };
+  ok = hipDeviceSynchronize() == hipSuccess && d2h(out->x, dout.x, B * N * 8) &&
+       d2h(out->iters, dout.iters, B * 4) && d2h(out->discr, dout.discr, B * M1 * 8) &&
+       (!out->times || d2h(out->times, dout.times, B * M1 * 8)) &&
+       (!out->crit || d2h(out->crit, dout.crit, B * M1 * 8)) &&
+       (!out->flags || d2h(out->flags, dout.flags, B * M1 * 4)) &&
+       (!out->beta_final || d2h(out->beta_final, dout.beta_final, B * 8)) &&
+       (!out->counters || d2h(out->counters, dout.counters, B * 32));
+  cleanup();
+  if (!ok) return fail(BSGP_ERR_HIP, "solve or device to host copy failed");
+  return BSGP_OK;
+}
+
+int bsgp_apply_operator(bsgp_plan p, int32_t B, int32_t transpose, const double* x, double* out,
+                        void* stream) {
+  if (!p || !x || !out || B < 1) return fail(BSGP_ERR_ARG, "bad arguments");
+  HIP_TRY(hipSetDevice(p->device));
+  const int grid = B < p->ncu * p->wg_per_cu ? B : p->ncu * p->wg_per_cu;
+  const size_t stride = round_up((size_t)p->g.H * p->g.Qh, 16);
+  if ((size_t)grid > p->opws_slots) {
+    if (p->opws) HIP_TRY(hipFree(p->opws));
+    p->opws = nullptr;
+    p->opws_slots = 0;
+    HIP_TRY(hipMalloc(&p->opws, (size_t)grid * stride * sizeof(cd)));
+    p->opws_slots = grid;
+  }
+  HIP_TRY(launch_apply_op(p->g, B, transpose, x, out, p->opws, stride, grid, p->lds_bytes,
+                          (hipStream_t)stream));
+  return BSGP_OK;
+}
+
+int bsgp_project_df(int64_t n, double b, const double* c, const double* dia, double scaling,
+                    int32_t has_sat, double ccd_sat_level, double lambda0, double dlambda0,
+                    double tol_lam, int32_t biter, int32_t siter, int32_t max_projs, double* x,
+                    double* info, void* stream) {
+  if (n < 1 || n > 0x7fffffff || !c || !dia || !x || !info)
+    return fail(BSGP_ERR_ARG, "bad arguments");
+  ProjClip clip{has_sat != 0, ccd_sat_level / scaling - 2.220446049250313e-16};
+  HIP_TRY(launch_project_df((int)n, b, c, dia, clip, lambda0, dlambda0, tol_lam, biter, siter,
+                            max_projs, x, info, (hipStream_t)stream));
+  return BSGP_OK;
+}
+
+int bsgp_beta_div(int64_t n, const double* y, const double* x, double beta, double* out,
+                  void* stream) {
+  if (n < 1 || n > 0x7fffffff || !y || !x || !out) return fail(BSGP_ERR_ARG, "bad arguments");
+  HIP_TRY(launch_beta_div((int)n, y, x, beta, out, (hipStream_t)stream));
+  return BSGP_OK;
+}
+
+int bsgp_beta_div_deriv(int64_t n, const double* y, const double* x, double beta, double* out,
+                        void* stream) {
+  if (n < 1 || !y || !x || !out) return fail(BSGP_ERR_ARG, "bad arguments");
+  HIP_TRY(launch_beta_div_deriv(n, y, x, beta, out, (hipStream_t)stream));
+  return BSGP_OK;
+}
+
+int bsgp_beta_div_grad_parts(int64_t n, const double* den, const double* gn, double beta,
+                             double* pow1, double* w, void* stream) {
+  if (n < 1 || !den || !gn || !pow1 || !w) return fail(BSGP_ERR_ARG, "bad arguments");
+  HIP_TRY(launch_grad_parts(n, den, gn, beta, pow1, w, (hipStream_t)stream));
+  return BSGP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,530 @@
+// bsgp_device.hpp — gfx950 device building blocks of the beta-SGP engine:
+// workgroup reductions, the three fused FFT-convolution passes, the
+// flux-conserving projection and the divergence terms.
+//
+// Execution model: one 512-thread workgroup (8 wavefronts) owns
+// one image for its whole solve.  All scalar control (projectDF's secant,
+// Armijo, Barzilai-Borwein, stop rules) is computed redundantly by every
+// thread from block-reduced sums, so no thread ever waits for a broadcast and
+// no host round trip exists inside a solve.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bsgp_fft.hpp"
+
+namespace bsgp {
+
+constexpr int kBlock = 512;
+constexpr int kWaves = kBlock / 64;
+constexpr int kMaxRed = 32;  // doubles reduced at once
+
+// Geometry of one conv plan (P x Q FFT grid, H x W image).
+struct Geo {
+  int H, W;      // image
+  int P, Q;      // FFT grid (circular: P=H, Q=W)
+  int Qh;        // stored half spectrum width = Q/2 + 1
+  int nfw;       // waves doing FFT work (each owns 2 LDS buffers)
+  int lpad;      // complex elements per LDS buffer (odd: spreads banks)
+  FftPlan fp;    // length P (columns)
+  FftPlan fq;    // length Q (rows)
+  const cd* tfA;   // [Qh][P] transfer function of A, scaled by 1/(P*Q)
+  const cd* tfAT;  // [Qh][P] transfer function of AT
+};
+
+// --------------------------------------------------------------- syncs
+// LDS hand-off between lanes of ONE wavefront: wait for this wave's LDS ops
+// and keep the compiler from moving LDS accesses across the point.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct WaveSync {
+  __device__ __forceinline__ void operator()() const { wave_sync(); }
+};
+
+// --------------------------------------------------------------- reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    double u = __shfl_xor(v, o, 64);
+    v = (u > v || u != u) ? u : v;  // NaN propagates like np.max
+  }
+  return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    double u = __shfl_xor(v, o, 64);
+    v = (u < v || u != u) ? u : v;
+  }
+  return v;
+}
+
+// Sum NV per-thread values over the workgroup; every thread gets the totals.
+// Fixed reduction order => deterministic, identical in every thread.
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
+  static_assert(NV <= kMaxRed, "too many values");
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    double s = wave_sum(v[i]);
+    if (lane == 0) red[w * kMaxRed + i] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    double s = red[i];
+    for (int k = 1; k < kWaves; ++k) s += red[k * kMaxRed + i];
+    v[i] = s;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ double block_max(double v, double* red) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  v = wave_max(v);
+  if (lane == 0) red[w * kMaxRed] = v;
+  __syncthreads();
+  double s = red[0];
+  for (int k = 1; k < kWaves; ++k) {
+    double u = red[k * kMaxRed];
+    s = (u > s || u != u) ? u : s;
+  }
+  __syncthreads();
+  return s;
+}
+
+__device__ __forceinline__ double block_min(double v, double* red) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  v = wave_min(v);
+  if (lane == 0) red[w * kMaxRed] = v;
+  __syncthreads();
+  double s = red[0];
+  for (int k = 1; k < kWaves; ++k) {
+    double u = red[k * kMaxRed];
+    s = (u < s || u != u) ? u : s;
+  }
+  __syncthreads();
+  return s;
+}
+
+// numpy-like max/min of two scalars (np.max([a, b]): NaN propagates)
+__device__ __forceinline__ double np_max2(double a, double b) {
+  return (a != a || b != b) ? (a + b) : (a > b ? a : b);
+}
+__device__ __forceinline__ double np_min2(double a, double b) {
+  return (a != a || b != b) ? (a + b) : (a < b ? a : b);
+}
+// Python builtin max(a, b) / min(a, b): first argument unless the second compares greater/less
+__device__ __forceinline__ double py_max2(double a, double b) { return (b > a) ? b : a; }
+__device__ __forceinline__ double py_min2(double a, double b) { return (b < a) ? b : a; }
+
+// --------------------------------------------------------------- conv passes
+// Spectrum scratch of one image: `nrows` rows x Qh complex, row-major.
+//
+// row_fwd: for every pair of image rows (r, r+1) one wave FFTs z = a + i b
+// (a, b real rows of length W zero-padded to Q) and stores the two half
+// spectra.  `prod(r, j)` produces the real input pixel (fused producer).
+template <class Prod>
+__device__ __forceinline__ void row_fwd(const Geo& G, int nrows, int ncols, cd* spec, cd* lds,
+                                        Prod&& prod) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (w < G.nfw) {
+    cd* a = lds + w * 2 * G.lpad;
+    cd* b = a + G.lpad;
+    for (int r = 2 * w; r < nrows; r += 2 * G.nfw) {
+      const bool two = (r + 1) < nrows;
+      for (int j = lane; j < G.Q; j += 64) {
+        double va = 0.0, vb = 0.0;
+        if (j < ncols) {
+          va = prod(r, j);
+          if (two) vb = prod(r + 1, j);
+        }
+        a[j] = cmk(va, vb);
+      }
+      wave_sync();
+      cd* Z = fft_run(a, b, G.fq, false, lane, 64, WaveSync());
+      cd* A = spec + (size_t)r * G.Qh;
+      for (int k = lane; k < G.Qh; k += 64) {
+        cd ak, bk;
+        r2c_split(Z, G.Q, k, &ak, &bk);
+        A[k] = ak;
+        if (two) A[G.Qh + k] = bk;
+      }
+      wave_sync();
+    }
+  }
+}
+
+// Rebuild the full-length row pair spectrum into `a` from stored half spectra.
+__device__ __forceinline__ void gather_pair(const Geo& G, const cd* A, bool two, cd* a, int lane) {
+  for (int k = lane; k < G.Q; k += 64) {
+    cd z;
+    if (two) {
+      z = c2r_gather(A, A + G.Qh, G.Q, G.Qh, k);
+    } else {
+      const cd v = (k < G.Qh) ? A[k] : cconj(A[G.Q - k]);
+      z = v;
+    }
+    a[k] = z;
+  }
+}
+
+// row_inv: inverse row transforms; `cons(r, j, value)` consumes each output
+// pixel (j < W) of rows [0, H).  The 1/(P*Q) scale is folded into the TF.
+template <class Cons>
+__device__ __forceinline__ void row_inv(const Geo& G, const cd* spec, cd* lds, Cons&& cons) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (w < G.nfw) {
+    cd* a = lds + w * 2 * G.lpad;
+    cd* b = a + G.lpad;
+    for (int r = 2 * w; r < G.H; r += 2 * G.nfw) {
+      const bool two = (r + 1) < G.H;
+      gather_pair(G, spec + (size_t)r * G.Qh, two, a, lane);
+      wave_sync();
+      cd* Z = fft_run(a, b, G.fq, true, lane, 64, WaveSync());
+      for (int j = lane; j < G.W; j += 64) {
+        const cd z = Z[j];
+        cons(r, j, z.x);
+        if (two) cons(r + 1, j, z.y);
+      }
+      wave_sync();
+    }
+  }
+}
+
+// row_inv_fwd: inverse rows of one convolution, then (same rows, same wave)
+// forward rows of the next one: `cp(r, j, value)` consumes the output pixel
+// and returns the next convolution's input pixel.  Spectrum rows are updated
+// in place.
+template <class CP>
+__device__ __forceinline__ void row_inv_fwd(const Geo& G, cd* spec, cd* lds, CP&& cp) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (w < G.nfw) {
+    cd* a = lds + w * 2 * G.lpad;
+    cd* b = a + G.lpad;
+    for (int r = 2 * w; r < G.H; r += 2 * G.nfw) {
+      const bool two = (r + 1) < G.H;
+      cd* A = spec + (size_t)r * G.Qh;
+      gather_pair(G, A, two, a, lane);
+      wave_sync();
+      cd* Z = fft_run(a, b, G.fq, true, lane, 64, WaveSync());
+      cd* in2 = (Z == a) ? b : a;
+      for (int j = lane; j < G.Q; j += 64) {
+        double va = 0.0, vb = 0.0;
+        if (j < G.W) {
+          const cd z = Z[j];
+          va = cp(r, j, z.x);
+          if (two) vb = cp(r + 1, j, z.y);
+        }
+        in2[j] = cmk(va, vb);
+      }
+      wave_sync();
+      cd* Y = fft_run(in2, Z, G.fq, false, lane, 64, WaveSync());
+      for (int k = lane; k < G.Qh; k += 64) {
+        cd ak, bk;
+        r2c_split(Y, G.Q, k, &ak, &bk);
+        A[k] = ak;
+        if (two) A[G.Qh + k] = bk;
+      }
+      wave_sync();
+    }
+  }
+}
+
+// col_conv: for every stored column k of the half spectrum, forward FFT over
+// the P-point column (rows >= H are the zero fill), multiply by tf[k][:],
+// inverse FFT, keep rows [0, H).  Columns are staged through LDS in tiles of
+// nfw columns with coalesced row-segment loads.
+__device__ __forceinline__ void col_conv(const Geo& G, cd* spec, const cd* tf, cd* lds) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int C = G.nfw;
+  const int stride = 2 * G.lpad;
+  for (int k0 = 0; k0 < G.Qh; k0 += C) {
+    for (int idx = threadIdx.x; idx < G.P * C; idx += kBlock) {
+      const int p = idx / C, c = idx - p * C, k = k0 + c;
+      cd v = cmk(0.0, 0.0);
+      if (p < G.H && k < G.Qh) v = spec[(size_t)p * G.Qh + k];
+      lds[c * stride + p] = v;
+    }
+    __syncthreads();
+    if (w < C && k0 + w < G.Qh) {
+      cd* a = lds + w * stride;
+      cd* b = a + G.lpad;
+      cd* Z = fft_run(a, b, G.fp, false, lane, 64, WaveSync());
+      const cd* t = tf + (size_t)(k0 + w) * G.P;
+      for (int p = lane; p < G.P; p += 64) Z[p] = cmul(Z[p], t[p]);
+      wave_sync();
+      cd* other = (Z == a) ? b : a;
+      cd* Y = fft_run(Z, other, G.fp, true, lane, 64, WaveSync());
+      if (Y != a) {
+        for (int p = lane; p < G.H; p += 64) a[p] = Y[p];
+        wave_sync();
+      }
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < G.H * C; idx += kBlock) {
+      const int p = idx / C, c = idx - p * C, k = k0 + c;
+      if (k < G.Qh) spec[(size_t)p * G.Qh + k] = lds[c * stride + p];
+    }
+    __syncthreads();
+  }
+}
+
+// --------------------------------------------------------------- projection
+// flux_conserve_proj.projectDF (flux_conserve_proj.py:7-144) for one image:
+// find lambda with |sum(x(lambda)) - b| <= 1e-11*b, x(lambda) =
+// min(max(0, (c + lambda)/dia), sat/scaling - eps).  `cdf(i, c, dia)` yields the
+// per-pixel (c, dia) on the fly.  Returns the final lambda; x(lambda) is
+// recomputed by the caller pixel by pixel (same arithmetic, same bits).
+struct ProjOut {
+  double lam;
+  int evals;
+  int biter;
+  int siter;
+};
+
+struct ProjClip {
+  bool has_sat;
+  double satv;  // ccd_sat_level/scaling - EPSILON
+  __device__ __forceinline__ double operator()(double c, double dia, double lam) const {
+    double v = (c + lam) / dia;
+    v = (0.0 > v) ? 0.0 : v;  // np.maximum(0, v) (NaN stays NaN)
+    if (has_sat) v = (satv < v) ? satv : v;  // np.minimum(satv, v)
+    return v;
+  }
+};
+
+template <class CDF>
+__device__ double proj_sum(int N, CDF& cdf, const ProjClip& clip, double lam, double* red) {
+  double s[1] = {0.0};
+  for (int i = threadIdx.x; i < N; i += kBlock) {
+    double c, dia;
+    cdf(i, c, dia);
+    s[0] += clip(c, dia, lam);
+  }
+  block_sum<1>(s, red);
+  return s[0];
+}
+
+template <class CDF>
+__device__ ProjOut project_df(int N, CDF&& cdf, const ProjClip& clip, double b, double lambda_,
+                              double dlambda_, double tol_lam, int biter, int siter,
+                              int max_projs, double* red) {
+  const int kCap = 200000;  // hard bound: the reference's r<0 bracket can spin forever
+  ProjOut o;
+  int nev = 0;
+  const double tol_r = 1e-11 * b;
+  double r = proj_sum(N, cdf, clip, lambda_, red) - b;
+  ++nev;
+  double lambdal = 0, lambdau = 0, rl = 0, ru = 0, s = 0;
+  if (fabs(r) < tol_r) goto done;
+  if (r < 0) {
+    lambdal = lambda_;
+    rl = r;
+    lambda_ = lambda_ + dlambda_;
+    r = proj_sum(N, cdf, clip, lambda_, red) - b;
+    ++nev;
+    while (r < 0 && nev < kCap) {
+      biter = biter + 1;
+      lambdal = lambda_;
+      s = np_max2(rl / r - 1, 0.1);
+      dlambda_ = dlambda_ + dlambda_ / s;
+      lambda_ = lambda_ + dlambda_;
+      rl = r;
+      r = proj_sum(N, cdf, clip, lambda_, red) - b;
+      ++nev;
+    }
+    lambdau = lambda_;
+    ru = r;
+  } else {
+    lambdau = lambda_;
+    ru = r;
+    lambda_ = lambda_ - dlambda_;
+    r = proj_sum(N, cdf, clip, lambda_, red) - b;
+    ++nev;
+    while (r > 0 && nev < kCap) {
+      biter = biter + 1;
+      lambdau = lambda_;
+      s = np_max2(ru / r - 1, 0.1);
+      // np.errstate(all='raise') around dlambda_ + dlambda_/s: overflow -> break
+      {
+        const double q = dlambda_ / s;
+        const double nd = dlambda_ + q;
+        const bool fin_in = isfinite(dlambda_) && isfinite(s);
+        if (fin_in && (!isfinite(q) || !isfinite(nd))) break;
+        if (fin_in && s == 0.0) break;
+        dlambda_ = nd;
+      }
+      lambda_ = lambda_ - dlambda_;
+      ru = r;
+      r = proj_sum(N, cdf, clip, lambda_, red) - b;
+      ++nev;
+    }
+    lambdal = lambda_;
+    rl = r;
+  }
+  if (fabs(ru) < tol_r) {
+    lambda_ = lambdau;
+    goto done;
+  }
+  if (fabs(rl) < tol_r) {
+    lambda_ = lambdal;
+    goto done;
+  }
+  s = 1 - rl / ru;
+  dlambda_ = dlambda_ / s;
+  lambda_ = lambdau - dlambda_;
+  r = proj_sum(N, cdf, clip, lambda_, red) - b;
+  ++nev;
+  {
+    const int maxit_s = max_projs - biter;
+    while (fabs(r) > tol_r && dlambda_ > tol_lam * (1 + fabs(lambda_)) && siter < maxit_s &&
+           nev < kCap) {
+      siter = siter + 1;
+      if (r > 0) {
+        if (s <= 2) {
+          lambdau = lambda_;
+          ru = r;
+          s = 1 - rl / ru;
+          dlambda_ = (lambdau - lambdal) / s;
+          lambda_ = lambdau - dlambda_;
+        } else {
+          s = np_max2(ru / r - 1, 0.1);
+          dlambda_ = (lambdau - lambda_) / s;
+          const double lambda_new = np_max2(lambda_ - dlambda_, 0.75 * lambdal + 0.25 * lambda_);
+          lambdau = lambda_;
+          ru = r;
+          lambda_ = lambda_new;
+          // flux_conserve_proj.py:122 assigns x, not s: s keeps the value above
+        }
+      } else {
+        if (s >= 2) {
+          lambdal = lambda_;
+          rl = r;
+          s = 1 - rl / ru;
+          dlambda_ = (lambdau - lambdal) / s;
+          lambda_ = lambdau - dlambda_;
+        } else {
+          s = np_max2(rl / r - 1, 0.1);
+          dlambda_ = (lambda_ - lambdal) / s;
+          const double lambda_new = np_min2(lambda_ + dlambda_, 0.75 * lambdau + 0.25 * lambda_);
+          lambdal = lambda_;
+          rl = r;
+          lambda_ = lambda_new;
+          s = (lambdau - lambdal) / (lambdau - lambda_);
+        }
+      }
+      r = proj_sum(N, cdf, clip, lambda_, red) - b;
+      ++nev;
+    }
+  }
+done:
+  o.lam = lambda_;
+  o.evals = nev;
+  o.biter = biter;
+  o.siter = siter;
+  return o;
+}
+
+// --------------------------------------------------------------- divergences
+// Objective of one line-search trial as (up to) three partial sums, combined
+// exactly as the reference combines its np.sum calls:
+//   KL   (sgp.py:334):      T0 = sum gn*log(gn/den), T1 = sum x_tf_try;  f = T0 + T1 - flux
+//   beta=0 (sgp.py:453):    T0 = sum gn/den, T1 = sum log(gn/den);        f = T0 - T1 - N
+//   beta=1 (sgp.py:455):    T0 = sum gn*log(gn/den), T1 = sum gn, T2 = sum den;  f = T0 - T1 + T2
+//   else  (sgp.py:457-458): T0 = sum s*gn^b, T1 = sum s(b-1)*den^b, T2 = sum s*b*gn*den^(b-1);
+//                           f = T0 + T1 - T2
+struct Objective {
+  int variant;  // 0 KL, 1 beta
+  double beta;
+  double scal, c1, c2;  // s, s*(b-1), s*b
+  int mode;             // 0 KL, 1 beta=0, 2 beta=1, 3 general
+  __device__ __forceinline__ void set_beta(double b) {
+    beta = b;
+    if (variant == 0) {
+      mode = 0;
+    } else if (b == 0.0) {
+      mode = 1;
+    } else if (b == 1.0) {
+      mode = 2;
+    } else {
+      mode = 3;
+      scal = 1 / (b * (b - 1));
+      c1 = scal * (b - 1);
+      c2 = scal * b;
+    }
+  }
+  // constant-in-lambda part for one pixel (mode 2: gn; mode 3: s*gn^b)
+  __device__ __forceinline__ double konst(double gnv) const {
+    if (mode == 2) return gnv;
+    if (mode == 3) return scal * pow(gnv, beta);
+    return 0.0;
+  }
+  // lambda-dependent parts for one pixel: adds to t[0..1]
+  __device__ __forceinline__ void terms(double xtf_try, double den, double gnv, double* t) const {
+    if (mode == 0) {
+      t[0] += gnv * log(gnv / den);
+      t[1] += xtf_try;
+    } else if (mode == 1) {
+      const double q = gnv / den;
+      t[0] += q;
+      t[1] += log(q);
+    } else if (mode == 2) {
+      t[0] += gnv * log(gnv / den);
+      t[1] += den;
+    } else {
+      const double p = pow(den, beta - 1);
+      t[0] += c1 * (den * p);
+      t[1] += (c2 * gnv) * p;
+    }
+  }
+  // f from the constant sum K and the two lambda sums
+  __device__ __forceinline__ double combine(double K, double t0, double t1, double flux,
+                                            double N) const {
+    if (mode == 0) return t0 + t1 - flux;
+    if (mode == 1) return t0 - t1 - N;
+    if (mode == 2) return t0 - K + t1;
+    return K + t0 - t1;
+  }
+  // gradient numerator w (input of AT) and the first gradient term g1:
+  // KL: g = 1 - AT(gn/den)               (sgp.py:263,342)
+  // beta: g = den^(b-1) - AT(gn*den^(b-2)) (sgp.py:498-499)
+  __device__ __forceinline__ double grad_w(double den, double gnv) const {
+    if (variant == 0) return gnv / den;
+    return gnv * (pow(den, beta - 1) / den);
+  }
+  __device__ __forceinline__ double grad_g1(double den) const {
+    if (variant == 0) return 1.0;
+    return pow(den, beta - 1);
+  }
+};
+
+// d betaDiv / d beta for one pixel (sgp.py:495), y = den, x = gn
+__device__ __forceinline__ double beta_deriv_px(double y, double x, double b) {
+  const double yb1 = pow(y, b - 1);
+  const double yb = pow(y, b);
+  const double xb = pow(x, b);
+  const double ly = log(y), lx = log(x);
+  double t = -x * yb1 * ly / (b - 1);
+  t = t + x * yb1 / ((b - 1) * (b - 1));
+  t = t + xb * lx / (b * (b - 1));
+  t = t - xb / (b * ((b - 1) * (b - 1)));
+  t = t + yb * ly / b;
+  t = t - xb / ((b * b) * (b - 1));
+  t = t - yb / (b * b);
+  return t;
+}
+
+}  // namespace bsgp

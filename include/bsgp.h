@@ -1,0 +1,153 @@
+/* bsgp.h — C ABI of the MI355X beta-SGP engine (libbsgp.so, gfx950).
+ *
+ * The reference boundary is a Python API, not an FFI: restoration/sgp.py's
+ * sgp() (sgp.py:41-47), sgp_betaDiv() (sgp.py:506-513), the betaDiv family
+ * (sgp.py:441-503) and flux_conserve_proj.projectDF() (flux_conserve_proj.py:7).
+ * The drop-in Python modules beta-sgp_amd/sgp.py and
+ * beta-sgp_amd/flux_conserve_proj.py keep those signatures and bind the entry
+ * points below through ctypes (INTEGRATION.md shows the stubs).
+ *
+ * Conventions
+ *  - plain C types only; device pointers are HBM buffers of the calling
+ *    process's current HIP device; `stream` is a hipStream_t passed as void*
+ *    (NULL = the null stream). Entry points are asynchronous on `stream`
+ *    unless their comment says otherwise.
+ *  - every function returns BSGP_OK (0) or a negative status; the message of
+ *    the last failure on the calling thread is in bsgp_last_error().
+ *  - all arrays are C-contiguous little-endian float64; an image batch is
+ *    [B][H][W].
+ *  - a plan is not thread-safe: one plan per device per host thread.
+ */
+#ifndef BSGP_H_
+#define BSGP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BSGP_OK 0
+#define BSGP_ERR_ARG (-1)          /* bad argument / shape                       */
+#define BSGP_ERR_HIP (-2)          /* a HIP runtime call failed                  */
+#define BSGP_ERR_UNSUPPORTED (-3)  /* geometry the kernels do not cover (yet)    */
+#define BSGP_ERR_PSF (-4)          /* PSF not normalised (sgp.py:97-102)         */
+
+/* conv_mode: which A/AT the solver uses.
+ *  BSGP_CONV_CIRCULAR    use_original_SGP_Afunction=True  (sgp.py:108-120):
+ *                        A(x)=Re ifft2(fft2(fftshift(psf)) . fft2(x)), AT uses conj;
+ *                        psf must have the image's shape.
+ *  BSGP_CONV_LINEAR_FILL use_original_SGP_Afunction=False (sgp.py:121-161):
+ *                        astropy convolve_fft(x, psf/sum(psf)) with zero fill,
+ *                        cropped; AT convolves with psf.T. */
+#define BSGP_CONV_CIRCULAR 0
+#define BSGP_CONV_LINEAR_FILL 1
+
+#define BSGP_VARIANT_KL 0   /* sgp()          sgp.py:41-438  */
+#define BSGP_VARIANT_BETA 1 /* sgp_betaDiv()  sgp.py:506-895 */
+
+typedef struct bsgp_plan_s* bsgp_plan;
+
+/* Every keyword argument of sgp()/sgp_betaDiv() that reaches the iteration.
+ * Field meanings are the reference's (sgp.py:48-77, 515-542). */
+typedef struct {
+  int32_t variant;        /* BSGP_VARIANT_*                                        */
+  int32_t init_recon;     /* 0 zeros, 1 x0 given (randn, sgp.py:169-170), 2 gn, 3 flat */
+  int32_t proj_type;      /* 0 clamp at 0, 1 flux-conserving projectDF             */
+  int32_t stop_criterion; /* 0/1 MAXIT only, 2 step norm, 3 rel. decrease, 4 discrepancy */
+  int32_t MAXIT;
+  int32_t M_alpha;        /* <= 32 */
+  int32_t M;              /* <= 32 */
+  int32_t max_projs;
+  double gamma, beta, alpha, alpha_min, alpha_max, tau;
+  double ccd_sat_level;   /* used when has_sat */
+  double betaParam, lr, lr_exp_param;
+  double tol_convergence;
+  double prescaled_scaling; /* scale_data == 2: the scaling the caller applied    */
+  double prescaled_tol4;    /* scale_data == 2 and stop_criterion 4: 1+1/mean(gn) */
+  int32_t has_sat;
+  int32_t scale_data;     /* 0 none, 1 scaling = max(gn) on device (sgp.py:193-199),
+                             2 inputs already scaled by the caller in their own dtype:
+                             gn, bkg, x0 are used as given (x0 required)          */
+  int32_t verbose;        /* only changes tol**2 for stop_criterion 2 (sgp.py:291-294) */
+  int32_t adapt_beta;
+  int32_t schedule_lr;
+  int32_t bkg_is_map;     /* bkg is [B][H][W] instead of [B] scalars               */
+  int32_t ls_spec;        /* line-search lambdas evaluated per pass (1..8); 1 when adapt_beta */
+  int32_t reserved;
+} bsgp_params;
+
+/* Device inputs of a batched solve. */
+typedef struct {
+  const double* gn;    /* [B][H][W] observed images (any scale; scaled on device) */
+  const double* bkg;   /* [B] or [B][H][W] (bkg_is_map)                           */
+  const double* flux;  /* [B] precomputed flux (unscaled) or NULL = sum(gn - bkg)  */
+  const double* x0;    /* [B][H][W] initial x (init_recon == 1, or scale_data == 2), else NULL */
+  const double* beta0; /* [B] per-image initial betaParam or NULL = params.betaParam */
+} bsgp_inputs;
+
+/* Device outputs of a batched solve.  MAXIT1 = MAXIT + 1. */
+typedef struct {
+  double* x;           /* [B][H][W] restored image (x * scaling)                  */
+  int32_t* iters;      /* [B] iterations (the reference's returned iter_)         */
+  double* discr;       /* [B][MAXIT1] discrepancy 2/N*scaling*f (sgp.py:276,392)  */
+  double* times;       /* [B][MAXIT1] seconds since solve start (sgp.py:391), may be NULL */
+  double* crit;        /* [B][MAXIT1] stop-rule value per iteration, may be NULL  */
+  int32_t* flags;      /* [B][MAXIT1] bit0: fv >= fr warning (sgp.py:351), may be NULL */
+  double* beta_final;  /* [B] final betaParam (sgp.py:892), may be NULL           */
+  int64_t* counters;   /* [B][4]: proj evals E_p, line-search evals E_ls,
+                          line-search passes, status bits; may be NULL             */
+} bsgp_outputs;
+
+/* Plan: geometry, FFT sizes, twiddles and the PSF transfer functions for A and
+ * AT, built on the device from the host PSF [kh][kw].  Synchronous. */
+int bsgp_plan_create(int32_t H, int32_t W, const double* psf_host, int32_t kh, int32_t kw,
+                     int32_t conv_mode, int32_t device, bsgp_plan* out);
+int bsgp_plan_destroy(bsgp_plan plan);
+/* FFT grid (P x Q) and the per-slot workspace bytes of the plan. */
+int bsgp_plan_info(bsgp_plan plan, int32_t* P, int32_t* Q, int64_t* slot_bytes,
+                   int32_t* fft_waves);
+
+/* Batched SGP / beta-SGP: B independent images (or (image, beta) candidates),
+ * each solved to completion by one persistent workgroup. Asynchronous. */
+int bsgp_solve_device(bsgp_plan plan, int32_t B, const bsgp_params* params,
+                      const bsgp_inputs* in, const bsgp_outputs* out, void* stream);
+
+/* Same with host buffers (copies in, solves, copies out). Synchronous. */
+int bsgp_solve_host(bsgp_plan plan, int32_t B, const bsgp_params* params,
+                    const bsgp_inputs* in, const bsgp_outputs* out);
+
+/* A (transpose=0) or AT (transpose=1) of the plan on B images. Asynchronous.
+ * Replaces the partial(afunction/A/AT, ...) operators of sgp.py:119-120,160-161. */
+int bsgp_apply_operator(bsgp_plan plan, int32_t B, int32_t transpose, const double* x,
+                        double* out, void* stream);
+
+/* flux_conserve_proj.projectDF(b, c, dia, scaling, ccd_sat_level, lambda_,
+ * dlambda_, tol_lam, biter, siter, max_projs) on one vector of length n.
+ * x: output [n]; info: output [4] = {final lambda, evaluations, biter, siter}.
+ * Asynchronous. */
+int bsgp_project_df(int64_t n, double b, const double* c, const double* dia, double scaling,
+                    int32_t has_sat, double ccd_sat_level, double lambda0, double dlambda0,
+                    double tol_lam, int32_t biter, int32_t siter, int32_t max_projs, double* x,
+                    double* info, void* stream);
+
+/* betaDiv(y, x, beta) (sgp.py:441-458) -> out[0]. Asynchronous. */
+int bsgp_beta_div(int64_t n, const double* y, const double* x, double beta, double* out,
+                  void* stream);
+/* betaDivDeriv(y, x, beta) elementwise (sgp.py:462-495) -> out[n]. Asynchronous. */
+int bsgp_beta_div_deriv(int64_t n, const double* y, const double* x, double beta, double* out,
+                        void* stream);
+/* The two elementwise parts of betaDivDerivwrtY (sgp.py:498-499):
+ * pow1 = den**(beta-1), w = gn*den**(beta-2). Asynchronous. */
+int bsgp_beta_div_grad_parts(int64_t n, const double* den, const double* gn, double beta,
+                             double* pow1, double* w, void* stream);
+
+int bsgp_device_synchronize(void);
+const char* bsgp_last_error(void);
+int32_t bsgp_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BSGP_H_ */
