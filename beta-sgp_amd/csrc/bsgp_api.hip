@@ -60,19 +60,30 @@ struct bsgp_plan_s {
   size_t ws_slots = 0;
   size_t slot_stride = 0;
   size_t vec_stride = 0;
-  int* queue = nullptr;
+  ImgState* st = nullptr;
+  size_t st_n = 0;
+  int* active = nullptr;     // device counter of images still iterating
+  int* active_h = nullptr;   // pinned host mirror for polling
   // operator workspace
   cd* opws = nullptr;
   size_t opws_slots = 0;
 };
 
 static int ensure_ws(bsgp_plan p, size_t slots) {
-  if (slots <= p->ws_slots) return BSGP_OK;
-  if (p->ws) HIP_TRY(hipFree(p->ws));
-  p->ws = nullptr;
-  p->ws_slots = 0;
-  HIP_TRY(hipMalloc(&p->ws, slots * p->slot_stride * sizeof(double)));
-  p->ws_slots = slots;
+  if (slots > p->ws_slots) {
+    if (p->ws) HIP_TRY(hipFree(p->ws));
+    p->ws = nullptr;
+    p->ws_slots = 0;
+    HIP_TRY(hipMalloc(&p->ws, slots * p->slot_stride * sizeof(double)));
+    p->ws_slots = slots;
+  }
+  if (slots > p->st_n) {
+    if (p->st) HIP_TRY(hipFree(p->st));
+    p->st = nullptr;
+    p->st_n = 0;
+    HIP_TRY(hipMalloc(&p->st, slots * sizeof(ImgState)));
+    p->st_n = slots;
+  }
   return BSGP_OK;
 }
 
@@ -136,11 +147,11 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   }
   int maxlen = g.P > g.Q ? g.P : g.Q;
   g.lpad = maxlen + 1;
-  // LDS: nfw waves x 2 buffers, + reduction scratch + queue slot
-  const size_t red_bytes = (size_t)kWaves * kMaxRed * sizeof(double) + 16;
+  // LDS: nfw waves x 2 buffers, + reduction scratch
+  const size_t red_bytes = (size_t)kWaves * kMaxRed * sizeof(double) + kSharedBytes;
   int nfw = kWaves;
-  size_t budget = 80 * 1024;  // two workgroups per CU
-  p->wg_per_cu = 2;
+  size_t budget = 160 * 1024 / 4 - 256;  // four workgroups per CU
+  p->wg_per_cu = 4;
   auto need = [&](int n) { return (size_t)n * 2 * g.lpad * sizeof(cd) + red_bytes; };
   while (nfw > 1 && need(nfw) > budget) nfw--;
   if (need(nfw) > budget) {
@@ -246,9 +257,10 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   const size_t N = (size_t)H * W;
   p->vec_stride = round_up(N, 32);
   p->slot_stride = 8 * p->vec_stride + round_up((size_t)H * g.Qh * 2, 32);
-  if (hipMalloc(&p->queue, 256) != hipSuccess) {
+  if (hipMalloc(&p->active, 256) != hipSuccess ||
+      hipHostMalloc(&p->active_h, 256, hipHostMallocDefault) != hipSuccess) {
     bsgp_plan_destroy(p);
-    return fail(BSGP_ERR_HIP, "queue allocation failed");
+    return fail(BSGP_ERR_HIP, "counter allocation failed");
   }
   *out = p;
   return BSGP_OK;
@@ -260,7 +272,9 @@ int bsgp_plan_destroy(bsgp_plan p) {
   if (p->tw) (void)hipFree(p->tw);
   if (p->tf) (void)hipFree(p->tf);
   if (p->ws) (void)hipFree(p->ws);
-  if (p->queue) (void)hipFree(p->queue);
+  if (p->st) (void)hipFree(p->st);
+  if (p->active) (void)hipFree(p->active);
+  if (p->active_h) (void)hipHostFree(p->active_h);
   if (p->opws) (void)hipFree(p->opws);
   delete p;
   return BSGP_OK;
@@ -301,8 +315,7 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     return fail(BSGP_ERR_ARG, "init_recon=1 and scale_data=2 need x0");
   if (!out || !out->x || !out->iters || !out->discr) return fail(BSGP_ERR_ARG, "outputs missing");
   HIP_TRY(hipSetDevice(p->device));
-  const int grid = B < p->ncu * p->wg_per_cu ? B : p->ncu * p->wg_per_cu;
-  rc = ensure_ws(p, (size_t)grid);
+  rc = ensure_ws(p, (size_t)B);
   if (rc) return rc;
   SolveArgs a;
   a.g = p->g;
@@ -310,14 +323,32 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   a.in = *in;
   a.out = *out;
   a.B = B;
-  a.queue = p->queue;
+  a.st = p->st;
+  a.active = p->active;
   a.ws = p->ws;
   a.slot_stride = p->slot_stride;
   a.vec_stride = p->vec_stride;
   a.lds_fft_bytes = p->lds_fft_bytes;
   hipStream_t s = (hipStream_t)stream;
-  HIP_TRY(hipMemsetAsync(p->queue, 0, 16, s));
-  HIP_TRY(launch_solve(a, grid, p->lds_bytes, s));
+  const int K = (prm->adapt_beta && prm->variant == BSGP_VARIANT_BETA)
+                    ? 1
+                    : (prm->ls_spec <= 1 ? 1 : prm->ls_spec <= 2 ? 2 : prm->ls_spec <= 4 ? 4 : 8);
+  // device counter of running images: every setup block adds one, every
+  // stopping image subtracts one (k_bb)
+  HIP_TRY(hipMemsetAsync(p->active, 0, 16, s));
+  HIP_TRY(launch_setup(a, p->lds_bytes, s));
+  // Fixed-length runs (stop_criterion 0/1) are launched back to back with no
+  // host synchronisation; data-dependent stop rules poll the counter.
+  const bool data_stop = prm->stop_criterion >= 2 && prm->stop_criterion <= 4;
+  const int poll = data_stop ? (B <= 4 ? 1 : 4) : 0;
+  for (int it = 1; it <= prm->MAXIT; ++it) {
+    HIP_TRY(launch_iteration(a, K, p->lds_bytes, s));
+    if (poll && it < prm->MAXIT && it % poll == 0) {
+      HIP_TRY(hipMemcpyAsync(p->active_h, p->active, sizeof(int), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      if (*p->active_h <= 0) break;
+    }
+  }
   return BSGP_OK;
 }
 

@@ -9,21 +9,35 @@
 
 namespace bsgp {
 
-// Everything one launch of the persistent solver needs (passed by value).
+// Per-image solver state carried between the phase kernels (device memory).
+struct ImgState {
+  int par, Xones, stop, iter, epoch, pad_;
+  int64_t E_p, E_ls, ls_passes, status;
+  double sc, flux, bks_scalar, lo, hi, Dcoeff, tol, t0;
+  double fv, alpha, tau, lr, init_lr, beta, lam_p, gd, lam;
+  double konst;  // lambda-independent objective sum at `beta` (sum s*gn^b / sum gn)
+  double Valpha[32];
+  double Fold[32];
+};
+
+// Everything a phase kernel needs (passed by value: kernel-argument loads are
+// scalar, so plan geometry and pointers stay in SGPRs).
 struct SolveArgs {
   Geo g;
   bsgp_params prm;
   bsgp_inputs in;
   bsgp_outputs out;
   int B;
-  int* queue;          // image dequeue counter, zeroed before the launch
-  double* ws;          // per-workgroup slots
+  ImgState* st;        // [B]
+  int* active;         // images still iterating
+  double* ws;          // per-image slots
   size_t slot_stride;  // doubles per slot
   size_t vec_stride;   // doubles per image vector (N rounded up to 32)
   size_t lds_fft_bytes;
 };
 
-hipError_t launch_solve(const SolveArgs& a, int grid, size_t lds, hipStream_t s);
+hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s);
+hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s);
 hipError_t launch_build_tf(const Geo& g, const double* kc, cd* spec, cd* tf, double scale,
                            int conj, size_t lds, hipStream_t s);
 hipError_t launch_apply_op(const Geo& g, int B, int transpose, const double* x, double* out,

@@ -4,9 +4,11 @@
 // Reference hot path: restoration/sgp.py:41-438 (sgp, KL) and :506-895
 // (sgp_betaDiv), restoration/flux_conserve_proj.py:7-144 (projectDF).
 //
-// One workgroup = one image for the whole solve (setup, every iteration,
-// every inner loop).  Workgroups pull images from a device queue, so a batch
-// of B images needs no host involvement between launch and completion.
+// One workgroup = one image in every phase kernel: setup, then per SGP
+// iteration k_dir (projection + direction + rows of d), k_col (columns with
+// A's transfer function), k_ls (line search + accept + rows of w), k_col (AT),
+// k_bb (gradient, x update, Barzilai-Borwein, stop rules).  All scalar
+// control runs on the device; per-image state lives in ImgState.
 #include <hip/hip_runtime.h>
 
 #include "bsgp_device.hpp"
@@ -25,435 +27,629 @@ __device__ __forceinline__ double realtime_s() {
   return (double)__builtin_amdgcn_s_memrealtime() * 1e-8;  // 100 MHz constant clock
 }
 
-// Per-image scalar state, identical in every thread of the workgroup.
-struct State {
-  double scaling, flux, fv, alpha, tau, lr, init_lr, beta;
-  double lo, hi;  // X bounds
-  double Valpha[32];
-  double Fold[32];
+// Streaming pass over pixel pairs [0, npair): every thread issues the loads of
+// U pairs before computing any of them (memory-level parallelism for one
+// workgroup streaming a whole image).  `ld(p)` loads, `cp(p, v)` computes.
+template <int U, class LD, class CP>
+__device__ __forceinline__ void stream2(int npair, LD&& ld, CP&& cp) {
+  using T = decltype(ld(0));
+  for (int b = threadIdx.x; b < npair; b += kBlock * U) {
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = b + u * kBlock;
+      if (p < npair) v[u] = ld(p);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = b + u * kBlock;
+      if (p < npair) cp(p, v[u]);
+    }
+  }
+}
+
+__device__ __forceinline__ double2 ld2(const double* a, int p) {
+  return reinterpret_cast<const double2*>(a)[p];
+}
+
+// Per-image slot vectors (x and g double-buffered; `par` picks the current
+// iterate).  Slot = image: state persists across the phase kernels.
+struct Bufs {
+  double *gns, *bks, *xa, *xb, *ga, *gb, *xtf, *dtf;
+  cd* spec;
 };
 
-// --------------------------------------------------------------- the solver
-__global__ void __launch_bounds__(kBlock) sgp_solve_kernel(SolveArgs A) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  cd* lds = reinterpret_cast<cd*>(smem);
-  double* red = reinterpret_cast<double*>(smem + A.lds_fft_bytes);
-  int& s_img = *reinterpret_cast<int*>(red + kWaves * kMaxRed);  // inside the dynamic carve
+__device__ __forceinline__ Bufs slot_bufs(const SolveArgs& A, int img, int par) {
+  Bufs b;
+  double* ws = A.ws + (size_t)img * A.slot_stride;
+  const size_t v = A.vec_stride;
+  b.gns = ws;
+  b.bks = ws + v;
+  double* x0 = ws + 2 * v;
+  double* x1 = ws + 3 * v;
+  double* g0 = ws + 4 * v;
+  double* g1 = ws + 5 * v;
+  b.xa = par ? x1 : x0;
+  b.xb = par ? x0 : x1;
+  b.ga = par ? g1 : g0;
+  b.gb = par ? g0 : g1;
+  b.xtf = ws + 6 * v;
+  b.dtf = ws + 7 * v;
+  b.spec = reinterpret_cast<cd*>(ws + 8 * v);
+  return b;
+}
 
+// The search direction of sgp.py:311-318 for one pixel: y = x - alpha*X*g,
+// projected (pflag 1: x(lambda_p) of projectDF(flux, y*D, D); pflag 0: y>=0).
+struct Dir {
+  bool Xones, proj;
+  double alpha, lo, hi, lam_p;
+  ProjClip clip;
+  __device__ __forceinline__ void cd_of(double x, double g, double& c, double& dia) const {
+    const double X = Xones ? 1.0 : clipX(x, lo, hi);
+    const double D = 1 / X;
+    const double y = x - alpha * (X * g);
+    c = y * D;
+    dia = D;
+  }
+  __device__ __forceinline__ double d(double x, double g) const {
+    double y;
+    if (proj) {
+      double c, dia;
+      cd_of(x, g, c, dia);
+      y = clip(c, dia, lam_p);
+    } else {
+      const double X = Xones ? 1.0 : clipX(x, lo, hi);
+      y = x - alpha * (X * g);
+      if (y < 0) y = 0;
+    }
+    return y - x;
+  }
+};
+
+__device__ __forceinline__ Dir make_dir(const SolveArgs& A, const ImgState& st) {
+  Dir D;
+  D.Xones = st.Xones != 0;
+  D.proj = A.prm.proj_type == 1;
+  D.alpha = st.alpha;
+  D.lo = st.lo;
+  D.hi = st.hi;
+  D.lam_p = st.lam_p;
+  D.clip = ProjClip{A.prm.has_sat != 0, A.prm.ccd_sat_level / st.sc - 2.220446049250313e-16};
+  return D;
+}
+
+__device__ __forceinline__ Objective make_obj(const SolveArgs& A, double beta) {
+  Objective o;
+  o.variant = A.prm.variant;
+  o.set_beta(beta);
+  return o;
+}
+
+#define BSGP_LDS_VIEWS(A)                                                           \
+  extern __shared__ __attribute__((aligned(16))) char smem[];                      \
+  cd* lds = reinterpret_cast<cd*>(smem);                                           \
+  double* red = reinterpret_cast<double*>(smem + (A).lds_fft_bytes)
+
+// ------------------------------------------------------------ kernel: setup
+// sgp.py:163-298 (= 617-742): scaling, null pixels, flux, x0, initial
+// projection, x_tf = A(x), f, g and the scaling-matrix bounds.
+__global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
+  BSGP_LDS_VIEWS(A);
+  const int img = blockIdx.x;
   const Geo& G = A.g;
   const bsgp_params& P = A.prm;
   const int N = G.H * G.W;
   const int tid = threadIdx.x;
   const bool bmap = P.bkg_is_map != 0;
-  const bool beta_v = P.variant == BSGP_VARIANT_BETA;
-  const int MAXIT1 = P.MAXIT + 1;
+  const bool odd = (N & 1) != 0;
+  Bufs B = slot_bufs(A, img, 0);
+  ImgState& st = A.st[img];
+  const double* gn_in = A.in.gn + (size_t)img * N;
+  const double* bk_in = bmap ? A.in.bkg + (size_t)img * N : nullptr;
+  const double bk_scalar_raw = bmap ? 0.0 : A.in.bkg[img];
+  const double t0 = realtime_s();
 
-  double* ws = A.ws + (size_t)blockIdx.x * A.slot_stride;
-  double* gns = ws;                 // scaled, null-fixed gn
-  double* bks = gns + A.vec_stride; // scaled bkg map (bmap)
-  double* xa = bks + A.vec_stride;  // x at iteration start
-  double* xb = xa + A.vec_stride;   // x at iteration end
-  double* ga = xb + A.vec_stride;
-  double* gb = ga + A.vec_stride;
-  double* xtf = gb + A.vec_stride;  // A(x)
-  double* dtf = xtf + A.vec_stride; // A(d)
-  cd* spec = reinterpret_cast<cd*>(dtf + A.vec_stride);
-
-  for (;;) {
-    if (tid == 0) s_img = atomicAdd(A.queue, 1);
-    __syncthreads();
-    const int img = s_img;
-    __syncthreads();
-    if (img >= A.B) break;
-
-    const double* gn_in = A.in.gn + (size_t)img * N;
-    const double* bk_in = bmap ? A.in.bkg + (size_t)img * N : nullptr;
-    const double bk_scalar_raw = bmap ? 0.0 : A.in.bkg[img];
-    const double t0 = realtime_s();
-
-    State S;
-    S.beta = A.in.beta0 ? A.in.beta0[img] : P.betaParam;
-    S.lr = P.lr;
-    S.init_lr = P.lr;
-    S.tau = P.tau;
-    S.alpha = P.alpha;
-    int64_t E_p = 0, E_ls = 0, ls_passes = 0, status = 0;
-
-    // ---- setup 1: raw statistics (sgp.py:174-177, 190, 193-194)
-    double sc;
-    {
-      double v[2] = {0.0, 0.0};  // sum(gn - bkg), sum(gn)
-      double mx = -INFINITY;
-      for (int i = tid; i < N; i += kBlock) {
-        const double g = gn_in[i];
-        const double bkr = bmap ? bk_in[i] : bk_scalar_raw;
-        v[0] += g - bkr;
-        v[1] += g;
-        mx = (g > mx || g != g) ? g : mx;
-      }
-      block_sum<2>(v, red);
-      mx = block_max(mx, red);
-      sc = P.scale_data == 2 ? P.prescaled_scaling : (P.scale_data ? mx : 1.0);
-      S.scaling = sc;
-      // init_recon 3 constant (before scaling), flux given or sum(gn - bkg)
-      const double flux_in = A.in.flux ? A.in.flux[img] : 0.0;
-      S.flux = A.in.flux ? flux_in : v[0];  // temporarily: raw flat-init numerator
-      S.fv = v[1] / (double)N;              // temporarily: mean(gn) for stop rule 4
+  // raw statistics (sgp.py:174-177, 190, 193-194)
+  double v2[2] = {0.0, 0.0};  // sum(gn - bkg), sum(gn)
+  double mx = -INFINITY;
+  for (int i = tid; i < N; i += kBlock) {
+    const double g = gn_in[i];
+    const double bkr = bmap ? bk_in[i] : bk_scalar_raw;
+    v2[0] += g - bkr;
+    v2[1] += g;
+    mx = (g > mx || g != g) ? g : mx;
+  }
+  block_sum<2>(v2, red);
+  mx = block_max(mx, red);
+  const double sc = P.scale_data == 2 ? P.prescaled_scaling : (P.scale_data ? mx : 1.0);
+  const double fl_raw = A.in.flux ? A.in.flux[img] : v2[0];
+  const double x3 = (fl_raw / (double)N) * 1.0;  // np.sum(gn-bkg)/gn.size*ones (sgp.py:175)
+  const double tol4 = P.scale_data == 2 ? P.prescaled_tol4 : 1 + 1 / (v2[1] / (double)N);
+  const bool divide = P.scale_data == 1;
+  const double bks_scalar = P.scale_data == 2 ? bk_scalar_raw : bk_scalar_raw / sc;
+  // scale + null-pixel minimum (sgp.py:193-204)
+  double vmin = INFINITY;
+  for (int i = tid; i < N; i += kBlock) {
+    const double g = divide ? gn_in[i] / sc : gn_in[i];
+    B.gns[i] = g;
+    if (g > 0 && g < vmin) vmin = g;
+    if (bmap) B.bks[i] = divide ? bk_in[i] / sc : bk_in[i];
+  }
+  vmin = block_min(vmin, red);
+  const double eps = 2.220446049250313e-16;
+  const double fill = vmin * eps * eps;
+  double v1[1] = {0.0};
+  for (int i = tid; i < N; i += kBlock) {
+    double g = B.gns[i];
+    if (g <= 0) {
+      g = fill;
+      B.gns[i] = g;
     }
-    const double x3 = (S.flux / (double)N) * 1.0;  // np.sum(gn-bkg)/gn.size*ones
-    const double tol4 = P.scale_data == 2 ? P.prescaled_tol4 : 1 + 1 / S.fv;
-    const bool divide = P.scale_data == 1;  // device applies the scaling
-    // ---- setup 2: scale, null-pixel minimum (sgp.py:193-204)
-    const double bks_scalar = P.scale_data == 2 ? bk_scalar_raw : bk_scalar_raw / sc;
-    {
-      double vmin = INFINITY;
-      for (int i = tid; i < N; i += kBlock) {
-        const double g = divide ? gn_in[i] / sc : gn_in[i];
-        gns[i] = g;
-        if (g > 0 && g < vmin) vmin = g;
-        if (bmap) bks[i] = divide ? bk_in[i] / sc : bk_in[i];
-      }
-      vmin = block_min(vmin, red);
-      const double eps = 2.220446049250313e-16;
-      const double fill = vmin * eps * eps;
-      double v[1] = {0.0};
-      for (int i = tid; i < N; i += kBlock) {
-        double g = gns[i];
-        if (g <= 0) {
-          g = fill;
-          gns[i] = g;
-        }
-        v[0] += g - (bmap ? bks[i] : bks_scalar);
-        // initial x (sgp.py:166-177, 197), then the pflag==0 clamp (:248-249)
-        double x;
-        if (A.in.x0) {
-          x = A.in.x0[(size_t)img * N + i];
-        } else if (P.init_recon == 0) {
-          x = 0.0;
-        } else if (P.init_recon == 2) {
-          x = gn_in[i];
-        } else {
-          x = x3;
-        }
-        if (divide) x = x / sc;
-        if (P.proj_type == 0 && x < 0) x = 0;
-        xa[i] = x;
-      }
-      block_sum<1>(v, red);
-      // flux (sgp.py:208-211)
-      S.flux = A.in.flux ? A.in.flux[img] / sc : v[0];
+    v1[0] += g - (bmap ? B.bks[i] : bks_scalar);
+    // initial x (sgp.py:166-177, 197), then the pflag==0 clamp (:248-249)
+    double x;
+    if (A.in.x0) {
+      x = A.in.x0[(size_t)img * N + i];
+    } else if (P.init_recon == 0) {
+      x = 0.0;
+    } else if (P.init_recon == 2) {
+      x = gn_in[i];
+    } else {
+      x = x3;
     }
-    const double flux = S.flux;
-    const ProjClip clip{P.has_sat != 0, P.ccd_sat_level / sc - 2.220446049250313e-16};
+    if (divide) x = x / sc;
+    if (P.proj_type == 0 && x < 0) x = 0;
+    B.xa[i] = x;
+  }
+  if (odd && tid == 0) {  // benign pad element of the pair-vectorised streams
+    B.gns[N] = 1.0;
+    if (bmap) B.bks[N] = 0.0;
+    B.xa[N] = B.xb[N] = B.ga[N] = B.gb[N] = B.xtf[N] = B.dtf[N] = 0.0;
+  }
+  block_sum<1>(v1, red);
+  const double flux = A.in.flux ? A.in.flux[img] / sc : v1[0];  // sgp.py:208-211
+  const ProjClip clip{P.has_sat != 0, P.ccd_sat_level / sc - eps};
+
+  // initial projection with dia = 1 (sgp.py:250-253)
+  if (P.proj_type == 1) {
+    ProjOut po = project_df(
+        N, [&](int i, double& c, double& dia) { c = B.xa[i]; dia = 1.0; }, clip, flux, 0.0, 1.0,
+        1e-11, 0, 0, P.max_projs, red);
+    for (int i = tid; i < N; i += kBlock) B.xa[i] = clip(B.xa[i], 1.0, po.lam);
     __syncthreads();
+  }
+  // x_tf = A(x), f and g (sgp.py:260-265 / 702-709)
+  const double beta0 = A.in.beta0 ? A.in.beta0[img] : P.betaParam;
+  Objective obj = make_obj(A, beta0);
+  double fsum[3] = {0.0, 0.0, 0.0};  // K, T0, T1
+  row_fwd(G, G.H, G.W, B.spec, lds, [&](int r, int j) { return B.xa[r * G.W + j]; });
+  __syncthreads();
+  col_conv(G, B.spec, G.tfA, lds);
+  row_inv_fwd(G, B.spec, lds, [&](int r, int j, double v) {
+    const int i = r * G.W + j;
+    B.xtf[i] = v;
+    const double den = v + (bmap ? B.bks[i] : bks_scalar);
+    const double g = B.gns[i];
+    fsum[0] += obj.konst(g);
+    obj.terms(v, den, g, &fsum[1]);
+    return obj.grad_w(den, g);
+  });
+  block_sum<3>(fsum, red);  // its barrier publishes xtf / spec
+  const double fv = obj.combine(fsum[0], fsum[1], fsum[2], flux, (double)N);
+  col_conv(G, B.spec, G.tfAT, lds);
+  row_inv(G, B.spec, lds, [&](int r, int j, double at) {
+    const int i = r * G.W + j;
+    const double den = B.xtf[i] + (bmap ? B.bks[i] : bks_scalar);
+    B.ga[i] = obj.grad_g1(den) - at;
+  });
+  __syncthreads();
+  // scaling-matrix bounds from AT(gn) (sgp.py:268-273)
+  row_fwd(G, G.H, G.W, B.spec, lds, [&](int r, int j) { return B.gns[r * G.W + j]; });
+  __syncthreads();
+  col_conv(G, B.spec, G.tfAT, lds);
+  double ymin = INFINITY, ymax = -INFINITY;
+  row_inv(G, B.spec, lds, [&](int r, int j, double at) {
+    const int i = r * G.W + j;
+    const double bkv = bmap ? B.bks[i] : bks_scalar;
+    const double y = (flux / (flux + bkv)) * at;
+    if (y > 0 && y < ymin) ymin = y;
+    ymax = (y > ymax || y != y) ? y : ymax;
+  });
+  ymin = block_min(ymin, red);
+  ymax = block_max(ymax, red);
+  double lo = ymin, hi = ymax;
+  if (hi / lo < 50) {
+    lo = lo / 10;
+    hi = hi * 10;
+  }
+  const double Dcoeff = 2 / (double)N * sc;
+  double tol = P.tol_convergence;
+  if (P.stop_criterion == 4) tol = tol4;
+  if (P.verbose && P.stop_criterion == 2) tol = tol * tol;
+  if (tid == 0) {
+    const int M1 = P.MAXIT + 1;
+    A.out.discr[(size_t)img * M1] = Dcoeff * fv;
+    if (A.out.times) A.out.times[(size_t)img * M1] = 0.0;
+    if (A.out.crit) A.out.crit[(size_t)img * M1] = 0.0;
+    if (A.out.flags) A.out.flags[(size_t)img * M1] = 0;
+    for (int k = 0; k < P.M_alpha; ++k) st.Valpha[k] = P.alpha_max;
+    for (int k = 0; k < P.M; ++k) st.Fold[k] = -1e30;
+    st.par = 0;
+    st.Xones = P.init_recon == 0;  // X = ones until the first BB update (sgp.py:279-280)
+    st.stop = 0;
+    st.iter = 1;
+    st.epoch = 0;
+    st.E_p = st.E_ls = st.ls_passes = st.status = 0;
+    st.sc = sc;
+    st.flux = flux;
+    st.bks_scalar = bks_scalar;
+    st.lo = lo;
+    st.hi = hi;
+    st.Dcoeff = Dcoeff;
+    st.tol = tol;
+    st.t0 = t0;
+    st.fv = fv;
+    st.alpha = P.alpha;
+    st.tau = P.tau;
+    st.lr = P.lr;
+    st.init_lr = P.lr;
+    st.beta = beta0;
+    st.konst = fsum[0];
+    atomicAdd(A.active, 1);
+  }
+}
 
-    // ---- setup 3: initial projection with dia = 1 (sgp.py:250-253)
-    if (P.proj_type == 1) {
-      ProjOut po = project_df(
-          N, [&](int i, double& c, double& dia) { c = xa[i]; dia = 1.0; }, clip, flux, 0.0, 1.0,
-          1e-11, 0, 0, P.max_projs, red);
-      for (int i = tid; i < N; i += kBlock) xa[i] = clip(xa[i], 1.0, po.lam);
-      __syncthreads();
-    }
-
-    // ---- setup 4: x_tf = A(x), f, g (sgp.py:260-265 / 702-709)
-    Objective obj;
-    obj.variant = P.variant;
-    obj.set_beta(S.beta);
-    double fsum[3] = {0.0, 0.0, 0.0};  // K, T0, T1
-    row_fwd(G, G.H, G.W, spec, lds, [&](int r, int j) { return xa[r * G.W + j]; });
-    __syncthreads();
-    col_conv(G, spec, G.tfA, lds);
-    row_inv_fwd(G, spec, lds, [&](int r, int j, double v) {
-      const int i = r * G.W + j;
-      xtf[i] = v;
-      const double den = v + (bmap ? bks[i] : bks_scalar);
-      const double g = gns[i];
-      fsum[0] += obj.konst(g);
-      obj.terms(v, den, g, &fsum[1]);
-      return obj.grad_w(den, g);
-    });
-    block_sum<3>(fsum, red);  // includes the barrier that publishes xtf / spec
-    S.fv = obj.combine(fsum[0], fsum[1], fsum[2], flux, (double)N);
-    col_conv(G, spec, G.tfAT, lds);
-    row_inv(G, spec, lds, [&](int r, int j, double at) {
-      const int i = r * G.W + j;
-      const double den = xtf[i] + (bmap ? bks[i] : bks_scalar);
-      ga[i] = obj.grad_g1(den) - at;
-    });
-    __syncthreads();
-    // ---- setup 5: scaling-matrix bounds from AT(gn) (sgp.py:268-273)
-    row_fwd(G, G.H, G.W, spec, lds, [&](int r, int j) { return gns[r * G.W + j]; });
-    __syncthreads();
-    col_conv(G, spec, G.tfAT, lds);
-    {
-      double ymin = INFINITY, ymax = -INFINITY;
-      row_inv(G, spec, lds, [&](int r, int j, double at) {
-        const int i = r * G.W + j;
-        const double bkv = bmap ? bks[i] : bks_scalar;
-        const double y = (flux / (flux + bkv)) * at;
-        if (y > 0 && y < ymin) ymin = y;
-        ymax = (y > ymax || y != y) ? y : ymax;
-      });
-      ymin = block_min(ymin, red);
-      ymax = block_max(ymax, red);
-      S.lo = ymin;
-      S.hi = ymax;
-      if (S.hi / S.lo < 50) {
-        S.lo = S.lo / 10;
-        S.hi = S.hi * 10;
-      }
-    }
-    const double Dcoeff = 2 / (double)N * sc;
-    double* discr = A.out.discr + (size_t)img * MAXIT1;
-    if (tid == 0) {
-      discr[0] = Dcoeff * S.fv;
-      if (A.out.times) A.out.times[(size_t)img * MAXIT1] = 0.0;
-      if (A.out.crit) A.out.crit[(size_t)img * MAXIT1] = 0.0;
-      if (A.out.flags) A.out.flags[(size_t)img * MAXIT1] = 0;
-    }
-    for (int k = 0; k < P.M_alpha; ++k) S.Valpha[k] = P.alpha_max;
-    for (int k = 0; k < P.M; ++k) S.Fold[k] = -1e30;
-    double tol = P.tol_convergence;
-    if (P.stop_criterion == 4) tol = tol4;
-    if (P.verbose && P.stop_criterion == 2) tol = tol * tol;
-    bool Xones = (P.init_recon == 0);  // X = ones until the first BB update (sgp.py:279-280)
-
-    // ---- main loop (sgp.py:302-425 / 748-882)
-    int iter_ = 1;
-    int epoch = 0;
-    const int K = P.adapt_beta && beta_v ? 1 : P.ls_spec;
-    for (;;) {
-      epoch += 1;
-      for (int k = 0; k < P.M_alpha - 1; ++k) S.Valpha[k] = S.Valpha[k + 1];
-      for (int k = 0; k < P.M - 1; ++k) S.Fold[k] = S.Fold[k + 1];
-      S.Fold[P.M - 1] = S.fv;
-      const double alpha = S.alpha;
-      const double lo = S.lo, hi = S.hi;
-
-      // direction y = x - alpha*X*g and its projection (sgp.py:311-316)
-      auto ycd = [&](int i, double& c, double& dia) {
-        const double x = xa[i];
-        const double X = Xones ? 1.0 : clipX(x, lo, hi);
-        const double D = 1 / X;
-        const double y = x - alpha * (X * ga[i]);
-        c = y * D;
-        dia = D;
-      };
-      double lam_p = 0.0;
-      if (P.proj_type == 1) {
-        ProjOut po = project_df(N, ycd, clip, flux, 0.0, 1.0, 1e-11, 0, 0, P.max_projs, red);
-        lam_p = po.lam;
-        E_p += po.evals;
-      }
-      auto dir = [&](int i) {  // d = y - x (sgp.py:318)
-        double y;
-        if (P.proj_type == 1) {
-          double c, dia;
-          ycd(i, c, dia);
-          y = clip(c, dia, lam_p);
-        } else {
-          const double x = xa[i];
-          const double X = Xones ? 1.0 : clipX(x, lo, hi);
-          y = x - alpha * (X * ga[i]);
-          if (y < 0) y = 0;
-        }
-        return y - xa[i];
-      };
-
-      // d, gd = d.g, A(d) (sgp.py:318-325)
-      double gd[1] = {0.0};
-      row_fwd(G, G.H, G.W, spec, lds, [&](int r, int j) {
-        const int i = r * G.W + j;
-        const double d = dir(i);
-        gd[0] += d * ga[i];
-        return d;
-      });
-      block_sum<1>(gd, red);
-      col_conv(G, spec, G.tfA, lds);
-
-      // line search (sgp.py:328-349 / 776-801): K trial lambdas per pass
-      double fr = S.Fold[0];
-      for (int k = 1; k < P.M; ++k) fr = py_max2(fr, S.Fold[k]);
-      double lam = 1.0;
-      int accepted = -1;
-      double f_acc = 0.0;
-      bool first = true;
-      int nls = 0;
-      while (accepted < 0) {
-        double lamk[8];
-        lamk[0] = lam;
-        for (int k = 1; k < K; ++k) lamk[k] = lamk[k - 1] * P.beta;
-        double t[2 * 8 + 2];
-        for (int k = 0; k < 2 * 8 + 2; ++k) t[k] = 0.0;
-        const bool adapt = P.adapt_beta && beta_v;
-        auto eval_px = [&](int i, double dt) {
-          const double g = gns[i];
-          const double bkv = bmap ? bks[i] : bks_scalar;
-          const double x0 = xtf[i];
-          t[2 * 8] += obj.konst(g);
-          for (int k = 0; k < K; ++k) {
-            const double xt = x0 + lamk[k] * dt;
-            const double den = xt + bkv;
-            obj.terms(xt, den, g, &t[2 * k]);
-          }
-          if (adapt) t[2 * 8 + 1] += beta_deriv_px(x0 + lamk[0] * dt + bkv, g, obj.beta);
-        };
-        if (first) {
-          row_inv(G, spec, lds, [&](int r, int j, double v) {
-            const int i = r * G.W + j;
-            dtf[i] = v;
-            eval_px(i, v);
+// ------------------------------------------ kernel: direction + rows of d
+// sgp.py:306-325: memory shifts, y = x - alpha*X*g, projectDF(flux, y*D, D)
+// with every x(lambda) evaluation one streaming pass over (x, g), d = y - x,
+// d.g, and the row transforms of d.
+__global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
+  BSGP_LDS_VIEWS(A);
+  const int img = blockIdx.x;
+  ImgState& st = A.st[img];
+  if (st.stop) return;
+  const Geo& G = A.g;
+  const bsgp_params& P = A.prm;
+  const int N = G.H * G.W;
+  const int npair = (N + 1) / 2;
+  const bool odd = (N & 1) != 0;
+  const int tid = threadIdx.x;
+  Bufs B = slot_bufs(A, img, st.par);
+  Dir D = make_dir(A, st);
+  int evals = 0;
+  if (P.proj_type == 1) {
+    const double* xa = B.xa;
+    const double* ga = B.ga;
+    auto psum = [&](double lam) {
+      double s[1] = {0.0};
+      stream2<4>(
+          npair,
+          [&](int p) {
+            struct V {
+              double2 x, g;
+            } v;
+            v.x = ld2(xa, p);
+            v.g = ld2(ga, p);
+            return v;
+          },
+          [&](int p, const auto& v) {
+            double c, d;
+            D.cd_of(v.x.x, v.g.x, c, d);
+            s[0] += D.clip(c, d, lam);
+            if (!odd || 2 * p + 1 < N) {
+              D.cd_of(v.x.y, v.g.y, c, d);
+              s[0] += D.clip(c, d, lam);
+            }
           });
-          first = false;
-        } else {
-          for (int i = tid; i < N; i += kBlock) eval_px(i, dtf[i]);
+      block_sum<1>(s, red);
+      return s[0];
+    };
+    ProjOut po = project_df_fn(psum, st.flux, 0.0, 1.0, 1e-11, 0, 0, P.max_projs);
+    D.lam_p = po.lam;
+    evals = po.evals;
+  }
+  double gd[1] = {0.0};
+  row_fwd(G, G.H, G.W, B.spec, lds, [&](int r, int j) {
+    const int i = r * G.W + j;
+    const double g = B.ga[i];
+    const double d = D.d(B.xa[i], g);
+    gd[0] += d * g;
+    return d;
+  });
+  block_sum<1>(gd, red);
+  if (tid == 0) {  // sgp.py:306-308 (memory shifts) + direction scalars
+    for (int k = 0; k < P.M_alpha - 1; ++k) st.Valpha[k] = st.Valpha[k + 1];
+    for (int k = 0; k < P.M - 1; ++k) st.Fold[k] = st.Fold[k + 1];
+    st.Fold[P.M - 1] = st.fv;
+    st.epoch += 1;
+    st.lam_p = D.lam_p;
+    st.E_p += evals;
+    st.gd = gd[0];
+  }
+}
+
+// ----------------------------------------------------------- kernel: columns
+__global__ void __launch_bounds__(kBlock) k_col(SolveArgs A, int transpose) {
+  BSGP_LDS_VIEWS(A);
+  const int img = blockIdx.x;
+  if (A.st[img].stop) return;
+  Bufs B = slot_bufs(A, img, 0);
+  col_conv(A.g, B.spec, transpose ? A.g.tfAT : A.g.tfA, lds);
+}
+
+// ------------------------------- kernel: line search + accept + rows of w
+// sgp.py:326-349 / 774-801: K trial lambdas per pass over (x_tf, d_tf, gn);
+// the first pass is fused into the inverse row transforms that produce d_tf.
+// Then x_tf += lam*d_tf and the row transforms of AT's input w.
+template <int K>
+__global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
+  // first pass (fused into the inverse rows of A(d)): one trial lambda = 1,
+  // which is where most non-stagnating iterations accept; later passes
+  // stream K trial lambdas each.
+  BSGP_LDS_VIEWS(A);
+  const int img = blockIdx.x;
+  ImgState& st = A.st[img];
+  if (st.stop) return;
+  const Geo& G = A.g;
+  const bsgp_params& P = A.prm;
+  const int N = G.H * G.W;
+  const int npair = (N + 1) / 2;
+  const bool odd = (N & 1) != 0;
+  const int tid = threadIdx.x;
+  const bool bmap = P.bkg_is_map != 0;
+  const bool adapt = P.adapt_beta && P.variant == BSGP_VARIANT_BETA;
+  Bufs B = slot_bufs(A, img, st.par);
+  const double bks_scalar = st.bks_scalar;
+  const double flux = st.flux;
+  const double gd = st.gd;
+  double fr = st.Fold[0];
+  for (int k = 1; k < P.M; ++k) fr = py_max2(fr, st.Fold[k]);
+  Objective obj = make_obj(A, st.beta);
+  double lam = 1.0;
+  double f_acc = 0.0;
+  int nls = 0, passes = 0, status = 0;
+  bool first = true;
+  constexpr int NT = 2 * K + 2;  // [2k],[2k+1]: lambda_k sums; [2K]: const; [2K+1]: dDiv/dbeta
+  // The lambda-independent sum (sum s*gn^b, or sum gn at beta = 1) is carried
+  // in the state; with adaptive beta it changes with beta and is recomputed.
+  double konst = st.konst;
+  for (;;) {
+    const int KK = first ? 1 : K;
+    double lamk[K];
+    lamk[0] = lam;
+#pragma unroll
+    for (int k = 1; k < K; ++k) lamk[k] = lamk[k - 1] * P.beta;
+    double t[NT];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) t[k] = 0.0;
+    if (first) {
+      double t1[4] = {0.0, 0.0, 0.0, 0.0};  // lambda = 1 sums, const, dDiv/dbeta
+      const double l0 = lamk[0];
+      row_inv(G, B.spec, lds, [&](int r, int j, double v) {
+        const int i = r * G.W + j;
+        B.dtf[i] = v;
+        const double g = B.gns[i];
+        const double x0 = B.xtf[i];
+        const double bkv = bmap ? B.bks[i] : bks_scalar;
+        const double xt = x0 + l0 * v;
+        obj.terms(xt, xt + bkv, g, &t1[0]);
+        if (adapt) {
+          t1[2] += obj.konst(g);
+          t1[3] += beta_deriv_px(xt + bkv, g, obj.beta);
         }
-        block_sum<2 * 8 + 2>(t, red);
-        ++ls_passes;
+      });
+      block_sum<4>(t1, red);
+      t[0] = t1[0];
+      t[1] = t1[1];
+      t[2 * K] = t1[2];
+      t[2 * K + 1] = t1[3];
+      first = false;
+    } else {
+      auto eval_px = [&](double x0, double dt, double g, double bkv) __attribute__((always_inline)) {
+        if (adapt) t[2 * K] += obj.konst(g);
+#pragma unroll
         for (int k = 0; k < K; ++k) {
-          const double fk = obj.combine(t[2 * 8], t[2 * k], t[2 * k + 1], flux, (double)N);
-          ++nls;
-          if (fk <= fr + P.gamma * lamk[k] * gd[0] || lamk[k] < 1e-12) {
-            accepted = k;
-            f_acc = fk;
-            lam = lamk[k];
-            break;
-          }
+          const double xt = x0 + lamk[k] * dt;
+          const double den = xt + bkv;
+          obj.terms(xt, den, g, &t[2 * k]);
         }
-        if (accepted < 0) {
-          lam = lamk[K - 1] * P.beta;
-          if (adapt) {  // sgp.py:798-800: beta -= lr * mean(dDiv/dbeta)
-            const double bgrad = (obj.beta == 0.0 || obj.beta == 1.0) ? 0.0 : t[2 * 8 + 1] / N;
-            obj.set_beta(obj.beta - S.lr * bgrad);
-          }
-        }
-        if (nls > 64) {  // unreachable: lam < 1e-12 forces acceptance by the 32nd trial
-          status |= 1;
-          accepted = 0;
-          f_acc = 0.0;
-        }
-      }
-      E_ls += nls;
-      S.fv = f_acc;
-      S.beta = obj.beta;
-      const double lam_acc = lam;
-      if (tid == 0 && A.out.flags)
-        A.out.flags[(size_t)img * MAXIT1 + iter_] = (S.fv >= fr) ? 1 : 0;
-
-      // accept: x_tf += lam*d_tf; w = gn/den or gn*den^(b-2); AT(w) (sgp.py:337-345)
-      row_fwd(G, G.H, G.W, spec, lds, [&](int r, int j) {
-        const int i = r * G.W + j;
-        const double xt = xtf[i] + lam_acc * dtf[i];
-        xtf[i] = xt;
-        const double den = xt + (bmap ? bks[i] : bks_scalar);
-        return obj.grad_w(den, gns[i]);
-      });
-      __syncthreads();
-      col_conv(G, spec, G.tfAT, lds);
-      // new gradient, x update, BB sums (sgp.py:337-365, 402)
-      double bb[6] = {0, 0, 0, 0, 0, 0};  // bk, ck, sk2.sk2, yk2.yk2, sk.sk, x.x
-      row_inv(G, spec, lds, [&](int r, int j, double at) {
-        const int i = r * G.W + j;
-        const double den = xtf[i] + (bmap ? bks[i] : bks_scalar);
-        const double gnew = obj.grad_g1(den) - at;
-        const double d = dir(i);
-        const double sk = lam_acc * d;
-        const double xn = xa[i] + lam_acc * d;
-        const double yk = gnew - ga[i];
-        const double X = clipX(xn, lo, hi);
-        const double D = 1 / X;
-        const double sk2 = sk * D;
-        const double yk2 = yk * X;
-        bb[0] += sk2 * yk;
-        bb[1] += yk2 * sk;
-        bb[2] += sk2 * sk2;
-        bb[3] += yk2 * yk2;
-        bb[4] += sk * sk;
-        bb[5] += xn * xn;
-        xb[i] = xn;
-        gb[i] = gnew;
-      });
-      block_sum<6>(bb, red);
-
-      // Barzilai-Borwein steps and the tau alternation (sgp.py:366-386)
-      double alpha1, alpha2;
-      if (bb[0] <= 0) {
-        alpha1 = py_min2(10 * alpha, P.alpha_max);
-      } else {
-        alpha1 = py_min2(P.alpha_max, py_max2(P.alpha_min, bb[2] / bb[0]));
-      }
-      if (bb[1] <= 0) {
-        alpha2 = py_min2(10 * alpha, P.alpha_max);
-      } else {
-        alpha2 = py_min2(P.alpha_max, py_max2(P.alpha_min, bb[1] / bb[3]));
-      }
-      S.Valpha[P.M_alpha - 1] = alpha2;
-      double vmin = S.Valpha[0];
-      for (int k = 1; k < P.M_alpha; ++k) vmin = py_min2(vmin, S.Valpha[k]);
-      if (iter_ <= 20) {
-        S.alpha = vmin;
-      } else if (alpha2 / alpha1 < S.tau) {
-        S.alpha = vmin;
-        S.tau = S.tau * 0.9;
-      } else {
-        S.alpha = alpha1;
-        S.tau = S.tau * 1.1;
-      }
-      if (beta_v && P.schedule_lr) S.lr = S.init_lr * exp(-P.lr_exp_param * epoch);
-
-      // stop rules (sgp.py:390-414)
-      iter_ += 1;
-      bool loop = true;
-      double crit = 0.0;
-      const double dk = Dcoeff * S.fv;
-      if (P.stop_criterion == 2) {
-        crit = bb[4] / bb[5];
-        loop = crit > tol;
-      } else if (P.stop_criterion == 3) {
-        crit = (S.Fold[P.M - 1] - S.fv) / S.fv;
-        loop = crit > tol && crit >= 0;
-      } else if (P.stop_criterion == 4) {
-        crit = dk;
-        loop = dk > tol;
-      }
-      if (iter_ > P.MAXIT) loop = false;
-      if (tid == 0) {
-        discr[iter_ - 1] = dk;
-        if (A.out.times) A.out.times[(size_t)img * MAXIT1 + iter_ - 1] = realtime_s() - t0;
-        if (A.out.crit) A.out.crit[(size_t)img * MAXIT1 + iter_ - 1] = crit;
-      }
-      if (!loop) break;  // x reverts to prev_x = xa (sgp.py:424-425)
-      double* t1 = xa;
-      xa = xb;
-      xb = t1;
-      t1 = ga;
-      ga = gb;
-      gb = t1;
-      Xones = false;
-      __syncthreads();
+        if (K == 1 && adapt) t[2 * K + 1] += beta_deriv_px(x0 + lamk[0] * dt + bkv, g, obj.beta);
+      };
+      const double* xtf = B.xtf;
+      const double* dtf = B.dtf;
+      const double* gns = B.gns;
+      const double* bks = B.bks;
+      stream2<1>(
+          npair,
+          [&](int p) {
+            struct V {
+              double2 x, d, g, b;
+            } v;
+            v.x = ld2(xtf, p);
+            v.d = ld2(dtf, p);
+            v.g = ld2(gns, p);
+            v.b = bmap ? ld2(bks, p) : double2{bks_scalar, bks_scalar};
+            return v;
+          },
+          [&](int p, const auto& v) {
+            eval_px(v.x.x, v.d.x, v.g.x, v.b.x);
+            if (!odd || 2 * p + 1 < N) eval_px(v.x.y, v.d.y, v.g.y, v.b.y);
+          });
+      block_sum<NT>(t, red);
     }
+    if (adapt) konst = t[2 * K];
+    ++passes;
+    int acc = -1;
+    for (int k = 0; k < KK; ++k) {
+      if (acc < 0) {
+        const double fk = obj.combine(konst, t[2 * k], t[2 * k + 1], flux, (double)N);
+        ++nls;
+        if (fk <= fr + P.gamma * lamk[k] * gd || lamk[k] < 1e-12) {
+          acc = k;
+          f_acc = fk;
+          lam = lamk[k];
+        }
+      }
+    }
+    if (acc >= 0) break;
+    lam = lamk[KK - 1] * P.beta;
+    if (adapt) {  // sgp.py:798-800: beta -= lr * mean(dDiv/dbeta)   (K == 1 here)
+      const double bgrad = (obj.beta == 0.0 || obj.beta == 1.0) ? 0.0 : t[2 * K + 1] / N;
+      obj.set_beta(obj.beta - st.lr * bgrad);
+    }
+    if (nls > 64) {  // unreachable: lam < 1e-12 forces acceptance by the 32nd trial
+      status = 1;
+      break;
+    }
+  }
+  // accept: x_tf += lam*d_tf; w = gn/den or gn*den^(b-2) (sgp.py:337-345, 790)
+  const double lam_acc = lam;
+  row_fwd(G, G.H, G.W, B.spec, lds, [&](int r, int j) {
+    const int i = r * G.W + j;
+    const double xt = B.xtf[i] + lam_acc * B.dtf[i];
+    B.xtf[i] = xt;
+    const double den = xt + (bmap ? B.bks[i] : bks_scalar);
+    return obj.grad_w(den, B.gns[i]);
+  });
+  if (tid == 0) {
+    if (A.out.flags)
+      A.out.flags[(size_t)img * (P.MAXIT + 1) + st.iter] = (f_acc >= fr) ? 1 : 0;
+    st.fv = f_acc;
+    st.beta = obj.beta;
+    st.konst = konst;
+    st.lam = lam_acc;
+    st.E_ls += nls;
+    st.ls_passes += passes;
+    st.status |= status;
+  }
+}
 
-    // ---- outputs (sgp.py:428-438, 892-895)
+// ------------------------------ kernel: gradient, x update, BB, stop rules
+// sgp.py:337-414 (= 785-879): g_new = g1(den) - AT(w), x += lam*d, the
+// Barzilai-Borwein step lengths with the tau alternation, the stop rules,
+// and the outputs once the image stops (sgp.py:424-438).
+__global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
+  BSGP_LDS_VIEWS(A);
+  const int img = blockIdx.x;
+  ImgState& st = A.st[img];
+  if (st.stop) return;
+  const Geo& G = A.g;
+  const bsgp_params& P = A.prm;
+  const int N = G.H * G.W;
+  const int tid = threadIdx.x;
+  const bool bmap = P.bkg_is_map != 0;
+  Bufs B = slot_bufs(A, img, st.par);
+  Dir D = make_dir(A, st);
+  const double lam = st.lam;
+  const double bks_scalar = st.bks_scalar;
+  Objective obj = make_obj(A, st.beta);
+  const double lo = st.lo, hi = st.hi;
+  double bb[6] = {0, 0, 0, 0, 0, 0};  // bk, ck, sk2.sk2, yk2.yk2, sk.sk, x.x
+  row_inv(G, B.spec, lds, [&](int r, int j, double at) {
+    const int i = r * G.W + j;
+    const double den = B.xtf[i] + (bmap ? B.bks[i] : bks_scalar);
+    const double gnew = obj.grad_g1(den) - at;
+    const double x = B.xa[i], g = B.ga[i];
+    const double d = D.d(x, g);
+    const double sk = lam * d;
+    const double xn = x + lam * d;
+    const double yk = gnew - g;
+    const double X = clipX(xn, lo, hi);
+    const double Dd = 1 / X;
+    const double sk2 = sk * Dd;
+    const double yk2 = yk * X;
+    bb[0] += sk2 * yk;
+    bb[1] += yk2 * sk;
+    bb[2] += sk2 * sk2;
+    bb[3] += yk2 * yk2;
+    bb[4] += sk * sk;
+    bb[5] += xn * xn;
+    B.xb[i] = xn;
+    B.gb[i] = gnew;
+  });
+  block_sum<6>(bb, red);
+  // Barzilai-Borwein (sgp.py:366-386)
+  const double alpha = st.alpha;
+  double alpha1, alpha2;
+  if (bb[0] <= 0) {
+    alpha1 = py_min2(10 * alpha, P.alpha_max);
+  } else {
+    alpha1 = py_min2(P.alpha_max, py_max2(P.alpha_min, bb[2] / bb[0]));
+  }
+  if (bb[1] <= 0) {
+    alpha2 = py_min2(10 * alpha, P.alpha_max);
+  } else {
+    alpha2 = py_min2(P.alpha_max, py_max2(P.alpha_min, bb[1] / bb[3]));
+  }
+  double vmin = P.M_alpha > 1 ? st.Valpha[0] : alpha2;  // python min(Valpha)
+  for (int k = 1; k < P.M_alpha - 1; ++k) vmin = py_min2(vmin, st.Valpha[k]);
+  if (P.M_alpha > 1) vmin = py_min2(vmin, alpha2);
+  const int iter = st.iter;
+  double tau = st.tau, anew;
+  if (iter <= 20) {
+    anew = vmin;
+  } else if (alpha2 / alpha1 < tau) {
+    anew = vmin;
+    tau = tau * 0.9;
+  } else {
+    anew = alpha1;
+    tau = tau * 1.1;
+  }
+  const double lr = (P.variant == BSGP_VARIANT_BETA && P.schedule_lr)
+                        ? st.init_lr * exp(-P.lr_exp_param * st.epoch)
+                        : st.lr;
+  // stop rules (sgp.py:390-414)
+  const int it2 = iter + 1;
+  bool loop = true;
+  double crit = 0.0;
+  const double fv = st.fv;
+  const double dk = st.Dcoeff * fv;
+  const double tol = st.tol;
+  if (P.stop_criterion == 2) {
+    crit = bb[4] / bb[5];
+    loop = crit > tol;
+  } else if (P.stop_criterion == 3) {
+    crit = (st.Fold[P.M - 1] - fv) / fv;
+    loop = crit > tol && crit >= 0;
+  } else if (P.stop_criterion == 4) {
+    crit = dk;
+    loop = dk > tol;
+  }
+  if (it2 > P.MAXIT) loop = false;
+  if (!loop) {
+    // outputs: x reverts to prev_x = xa (sgp.py:424-438, 892-895)
+    const double sc = st.sc;
     double* xo = A.out.x + (size_t)img * N;
-    for (int i = tid; i < N; i += kBlock) xo[i] = xa[i] * sc;
-    if (tid == 0) {
-      A.out.iters[img] = iter_ - 1;
-      if (A.out.beta_final) A.out.beta_final[img] = S.beta;
+    for (int i = tid; i < N; i += kBlock) xo[i] = B.xa[i] * sc;
+  }
+  __syncthreads();  // every thread has read st before thread 0 rewrites it
+  if (tid == 0) {
+    const size_t M1 = (size_t)P.MAXIT + 1;
+    A.out.discr[img * M1 + it2 - 1] = dk;
+    if (A.out.times) A.out.times[img * M1 + it2 - 1] = realtime_s() - st.t0;
+    if (A.out.crit) A.out.crit[img * M1 + it2 - 1] = crit;
+    st.Valpha[P.M_alpha - 1] = alpha2;
+    st.alpha = anew;
+    st.tau = tau;
+    st.lr = lr;
+    st.iter = it2;
+    if (loop) {
+      st.par ^= 1;
+      st.Xones = 0;
+    } else {
+      st.stop = 1;
+      A.out.iters[img] = it2 - 1;
+      if (A.out.beta_final) A.out.beta_final[img] = st.beta;
       if (A.out.counters) {
         int64_t* c = A.out.counters + (size_t)img * 4;
-        c[0] = E_p;
-        c[1] = E_ls;
-        c[2] = ls_passes;
-        c[3] = status;
+        c[0] = st.E_p;
+        c[1] = st.E_ls;
+        c[2] = st.ls_passes;
+        c[3] = st.status;
       }
+      atomicSub(A.active, 1);
     }
-    // restore slot pointers for the next image of this workgroup
-    xa = bks + A.vec_stride;
-    xb = xa + A.vec_stride;
-    ga = xb + A.vec_stride;
-    gb = ga + A.vec_stride;
-    __syncthreads();
   }
 }
 
@@ -513,7 +709,7 @@ __global__ void __launch_bounds__(kBlock) project_df_kernel(int n, double b, con
                                                             double tol_lam, int biter, int siter,
                                                             int max_projs, double* x,
                                                             double* info) {
-  __shared__ double red[kWaves * kMaxRed];
+  __shared__ double red[(kWaves + 1) * kMaxRed];
   ProjOut po = project_df(
       n, [&](int i, double& cc, double& dd) { cc = c[i]; dd = dia[i]; }, clip, b, lam0, dlam0,
       tol_lam, biter, siter, max_projs, red);
@@ -530,7 +726,7 @@ __global__ void __launch_bounds__(kBlock) project_df_kernel(int n, double b, con
 __global__ void __launch_bounds__(kBlock) beta_div_kernel(int n, const double* y,
                                                           const double* x, double beta,
                                                           double* out) {
-  __shared__ double red[kWaves * kMaxRed];
+  __shared__ double red[(kWaves + 1) * kMaxRed];
   Objective o;
   o.variant = 1;
   o.set_beta(beta);
@@ -560,8 +756,22 @@ __global__ void grad_parts_kernel(int64_t n, const double* den, const double* gn
 }
 
 // ----------------------------------------------------------- launchers
-hipError_t launch_solve(const SolveArgs& a, int grid, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL(sgp_solve_kernel, dim3(grid), dim3(kBlock), lds, s, a);
+hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL(k_setup, dim3(a.B), dim3(kBlock), lds, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
+  const dim3 grid(a.B), block(kBlock);
+  hipLaunchKernelGGL(k_dir, grid, block, lds, s, a);
+  hipLaunchKernelGGL(k_col, grid, block, lds, s, a, 0);
+  switch (K) {
+    case 1: hipLaunchKernelGGL(k_ls<1>, grid, block, lds, s, a); break;
+    case 2: hipLaunchKernelGGL(k_ls<2>, grid, block, lds, s, a); break;
+    case 4: hipLaunchKernelGGL(k_ls<4>, grid, block, lds, s, a); break;
+    default: hipLaunchKernelGGL(k_ls<8>, grid, block, lds, s, a); break;
+  }
+  hipLaunchKernelGGL(k_col, grid, block, lds, s, a, 1);
+  hipLaunchKernelGGL(k_bb, grid, block, lds, s, a);
   return hipGetLastError();
 }
 hipError_t launch_build_tf(const Geo& g, const double* kc, cd* spec, cd* tf, double scale,
@@ -603,14 +813,15 @@ hipError_t launch_grad_parts(int64_t n, const double* den, const double* gn, dou
   return hipGetLastError();
 }
 hipError_t set_solver_lds_limit(size_t bytes) {
-  hipError_t e = hipFuncSetAttribute((const void*)sgp_solve_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)apply_op_kernel,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)build_tf_kernel,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  const void* fns[] = {(const void*)k_setup,     (const void*)k_dir,       (const void*)k_col,
+                       (const void*)k_ls<1>,     (const void*)k_ls<2>,     (const void*)k_ls<4>,
+                       (const void*)k_ls<8>,     (const void*)k_bb,        (const void*)apply_op_kernel,
+                       (const void*)build_tf_kernel};
+  for (const void* f : fns) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace bsgp

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Print VGPR / spill / scratch of every kernel in bsgp_solver.hip (gfx950).
+set -e
+R=$(cd "$(dirname "$0")/.." && pwd)
+D=$(mktemp -d)
+cd $D
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -mcode-object-version=5 \
+  -I $R/include -c $R/beta-sgp_amd/csrc/bsgp_solver.hip -o s.o -save-temps "$@" 2>/dev/null
+python3 - <<'PY'
+import re
+s=open('bsgp_solver-hip-amdgcn-amd-amdhsa-gfx950.s').read()
+for m in re.finditer(r'\.name:\s+(\S+)\n(.*?)(?=\n  - \.|\Z)', s, re.S):
+    pass
+blocks=s.split('.name:')
+for b in blocks[1:]:
+    name=b.split()[0]
+    def g(k):
+        m=re.search(r'\.'+k+r':\s+(\d+)', b); return m.group(1) if m else '?'
+    print(f"{name[:60]:60s} vgpr={g('vgpr_count')} spill={g('vgpr_spill_count')} scratch={g('private_segment_fixed_size')} sgpr={g('sgpr_count')}")
+PY
+rm -rf $D
