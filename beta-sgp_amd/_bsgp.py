@@ -50,7 +50,7 @@ class Params(ctypes.Structure):
         ("prescaled_tol4", ctypes.c_double),
         ("has_sat", ctypes.c_int32), ("scale_data", ctypes.c_int32), ("verbose", ctypes.c_int32),
         ("adapt_beta", ctypes.c_int32), ("schedule_lr", ctypes.c_int32),
-        ("bkg_is_map", ctypes.c_int32), ("ls_spec", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("bkg_is_map", ctypes.c_int32), ("ls_spec", ctypes.c_int32), ("ls_series", ctypes.c_int32),
     ]
 
 
@@ -189,7 +189,7 @@ class Plan:
             "crit": torch.zeros(B, M1, **f64),
             "flags": torch.zeros(B, M1, dtype=torch.int32, device=dev),
             "beta_final": torch.zeros(B, **f64),
-            "counters": torch.zeros(B, 4, dtype=torch.int64, device=dev),
+            "counters": torch.zeros(B, 8, dtype=torch.int64, device=dev),
         }
         ins = Inputs(_ptr(gn), _ptr(bkg), _ptr(flux), _ptr(x0), _ptr(beta0))
         outs = Outputs(*[_ptr(out[k]) for k in ["x", "iters", "discr", "times", "crit", "flags",

@@ -386,7 +386,7 @@ int bsgp_solve_host(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_i
   if (out->crit) dout.crit = (double*)dalloc(B * M1 * 8);
   if (out->flags) dout.flags = (int32_t*)dalloc(B * M1 * 4);
   if (out->beta_final) dout.beta_final = (double*)dalloc(B * 8);
-  if (out->counters) dout.counters = (int64_t*)dalloc(B * 4 * 8);
+  if (out->counters) dout.counters = (int64_t*)dalloc(B * 8 * 8);
   for (void* b : bufs)
     if (!b) {
       cleanup();
@@ -418,7 +418,7 @@ int bsgp_solve_host(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_i
        (!out->crit || d2h(out->crit, dout.crit, B * M1 * 8)) &&
        (!out->flags || d2h(out->flags, dout.flags, B * M1 * 4)) &&
        (!out->beta_final || d2h(out->beta_final, dout.beta_final, B * 8)) &&
-       (!out->counters || d2h(out->counters, dout.counters, B * 32));
+       (!out->counters || d2h(out->counters, dout.counters, B * 64));
   cleanup();
   if (!ok) return fail(BSGP_ERR_HIP, "solve or device to host copy failed");
   return BSGP_OK;

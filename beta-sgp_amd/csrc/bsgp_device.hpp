@@ -15,6 +15,7 @@
 #include <type_traits>
 
 #include "bsgp_fft.hpp"
+#include "bsgp_math.hpp"
 
 namespace bsgp {
 
@@ -131,11 +132,11 @@ __device__ __forceinline__ double block_min(double v, double* red) {
   return s;
 }
 
-// x**a for the divergence terms: exp(a*log(x)).  For the beta values of this
-// path (|a| = |beta-1| <~ 1, scaled data so |log x| <~ 20) the error is a few
-// ulp at most, against ~2x the cost for the general pow(); x <= 0 follows pow
-// for the cases the iteration can produce (0 -> 0 or inf, negative -> NaN).
-__device__ __forceinline__ double fpow(double x, double a) { return exp(a * log(x)); }
+// x**a for the divergence terms: exp(a*fast_log(x)) (bsgp_math.hpp).  For the
+// exponents of this path (|a| = |beta-1| <~ 1, scaled data so |log x| <~ 20)
+// the error is a few ulp at most, at ~1/2.6 the cost of the general pow();
+// x <= 0 follows pow for the cases the iteration can produce.
+__device__ __forceinline__ double fpow(double x, double a) { return exp(a * fast_log(x)); }
 
 // numpy-like max/min of two scalars (np.max([a, b]): NaN propagates)
 __device__ __forceinline__ double np_max2(double a, double b) {
@@ -505,14 +506,14 @@ struct Objective {
   // lambda-dependent parts for one pixel: adds to t[0..1]
   __device__ __forceinline__ void terms(double xtf_try, double den, double gnv, double* t) const {
     if (mode == 0) {
-      t[0] += gnv * log(gnv / den);
+      t[0] += gnv * fast_log(gnv / den);
       t[1] += xtf_try;
     } else if (mode == 1) {
       const double q = gnv / den;
       t[0] += q;
-      t[1] += log(q);
+      t[1] += fast_log(q);
     } else if (mode == 2) {
-      t[0] += gnv * log(gnv / den);
+      t[0] += gnv * fast_log(gnv / den);
       t[1] += den;
     } else {
       const double p = fpow(den, beta - 1);
@@ -543,10 +544,10 @@ struct Objective {
 
 // d betaDiv / d beta for one pixel (sgp.py:495), y = den, x = gn
 __device__ __forceinline__ double beta_deriv_px(double y, double x, double b) {
-  const double yb1 = pow(y, b - 1);
-  const double yb = pow(y, b);
-  const double xb = pow(x, b);
-  const double ly = log(y), lx = log(x);
+  const double ly = fast_log(y), lx = fast_log(x);
+  const double yb1 = exp((b - 1) * ly);
+  const double yb = exp(b * ly);
+  const double xb = exp(b * lx);
   double t = -x * yb1 * ly / (b - 1);
   t = t + x * yb1 / ((b - 1) * (b - 1));
   t = t + xb * lx / (b * (b - 1));

@@ -12,7 +12,7 @@ namespace bsgp {
 // Per-image solver state carried between the phase kernels (device memory).
 struct ImgState {
   int par, Xones, stop, iter, epoch, pad_;
-  int64_t E_p, E_ls, ls_passes, status;
+  int64_t E_p, E_ls, ls_passes, status, ls_series;
   double sc, flux, bks_scalar, lo, hi, Dcoeff, tol, t0;
   double fv, alpha, tau, lr, init_lr, beta, lam_p, gd, lam;
   double konst;  // lambda-independent objective sum at `beta` (sum s*gn^b / sum gn)

@@ -280,7 +280,7 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     st.stop = 0;
     st.iter = 1;
     st.epoch = 0;
-    st.E_p = st.E_ls = st.ls_passes = st.status = 0;
+    st.E_p = st.E_ls = st.ls_passes = st.status = st.ls_series = 0;
     st.sc = sc;
     st.flux = flux;
     st.bks_scalar = bks_scalar;
@@ -408,14 +408,117 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
   Objective obj = make_obj(A, st.beta);
   double lam = 1.0;
   double f_acc = 0.0;
-  int nls = 0, passes = 0, status = 0;
-  bool first = true;
+  int nls = 0, passes = 0, status = 0, series_evals = 0;
+  bool accepted = false;
   constexpr int NT = 2 * K + 2;  // [2k],[2k+1]: lambda_k sums; [2K]: const; [2K+1]: dDiv/dbeta
   // The lambda-independent sum (sum s*gn^b, or sum gn at beta = 1) is carried
   // in the state; with adaptive beta it changes with beta and is recomputed.
   double konst = st.konst;
-  for (;;) {
-    const int KK = first ? 1 : K;
+  // Small-step series (general beta, fixed beta): with den_i(lam) =
+  // a_i (1 + lam u_i), a_i = x_tf_i + bkg_i, u_i = d_tf_i / a_i,
+  //   sum den^b        = sum_m binom(b, m)   lam^m P_m,  P_m = sum a^b u^m
+  //   sum gn den^(b-1) = sum_m binom(b-1, m) lam^m Q_m,  Q_m = sum gn a^(b-1) u^m
+  // so every trial with lam * max|u| <= kSeriesRho is evaluated without a pass
+  // over the image (truncation < 1e-17 relative at MS = 8).
+  constexpr int MS = 8;
+  constexpr double kSeriesRho = 0.01;
+  const bool series = P.ls_series != 0 && !adapt && obj.mode == 3;
+  double Pm[MS + 1], Qm[MS + 1];
+  double rho = INFINITY;
+  // ---- pass 1, fused into the inverse rows that produce d_tf: lam = 1 direct
+  {
+    constexpr int N1 = 4 + 2 * (MS + 1);  // lam=1 sums, const, dDiv/dbeta, P_m, Q_m
+    double t1[N1];
+#pragma unroll
+    for (int k = 0; k < N1; ++k) t1[k] = 0.0;
+    double umax = 0.0;
+    row_inv(G, B.spec, lds, [&](int r, int j, double v) {
+      const int i = r * G.W + j;
+      B.dtf[i] = v;
+      const double g = B.gns[i];
+      const double x0 = B.xtf[i];
+      const double bkv = bmap ? B.bks[i] : bks_scalar;
+      const double xt = x0 + lam * v;
+      obj.terms(xt, xt + bkv, g, &t1[0]);
+      if (adapt) {
+        t1[2] += obj.konst(g);
+        t1[3] += beta_deriv_px(xt + bkv, g, obj.beta);
+      }
+      if (series) {
+        const double a = x0 + bkv;
+        const double u = v / a;
+        const double p0 = fpow(a, obj.beta - 1);
+        const double A0 = a * p0, B0 = g * p0;
+        double um = 1.0;
+#pragma unroll
+        for (int m = 0; m <= MS; ++m) {
+          t1[4 + m] += A0 * um;
+          t1[4 + MS + 1 + m] += B0 * um;
+          um *= u;
+        }
+        const double au = fabs(u);
+        umax = (au > umax || au != au || !(a > 0)) ? (a > 0 ? au : INFINITY) : umax;
+      }
+    });
+    block_sum<N1>(t1, red);
+    if (series) rho = block_max(umax, red);
+#pragma unroll
+    for (int m = 0; m <= MS; ++m) {
+      Pm[m] = t1[4 + m];
+      Qm[m] = t1[4 + MS + 1 + m];
+    }
+    if (adapt) konst = t1[2];
+    ++passes;
+    ++nls;
+    const double f1 = obj.combine(konst, t1[0], t1[1], flux, (double)N);
+    if (f1 <= fr + P.gamma * lam * gd || lam < 1e-12) {
+      f_acc = f1;
+      accepted = true;
+    } else {
+      lam = lam * P.beta;
+      if (adapt) {  // sgp.py:798-800: beta -= lr * mean(dDiv/dbeta)
+        const double bgrad = (obj.beta == 0.0 || obj.beta == 1.0) ? 0.0 : t1[3] / N;
+        obj.set_beta(obj.beta - st.lr * bgrad);
+      }
+    }
+  }
+  // binomial coefficients of the series
+  double cb[MS + 1], cb1[MS + 1];
+  if (series) {
+    cb[0] = 1.0;
+    cb1[0] = 1.0;
+#pragma unroll
+    for (int m = 1; m <= MS; ++m) {
+      cb[m] = cb[m - 1] * (obj.beta - (m - 1)) / m;
+      cb1[m] = cb1[m - 1] * (obj.beta - 1 - (m - 1)) / m;
+    }
+  }
+  while (!accepted) {
+    if (series && lam * rho <= kSeriesRho) {
+      // closed-form trial: no pass over the image
+      double s0 = 0.0, s1 = 0.0, lm = 1.0;
+#pragma unroll
+      for (int m = 0; m <= MS; ++m) {
+        s0 += cb[m] * lm * Pm[m];
+        s1 += cb1[m] * lm * Qm[m];
+        lm *= lam;
+      }
+      const double fk = obj.combine(konst, obj.c1 * s0, obj.c2 * s1, flux, (double)N);
+      ++nls;
+      ++series_evals;
+      if (fk <= fr + P.gamma * lam * gd || lam < 1e-12) {
+        f_acc = fk;
+        accepted = true;
+        break;
+      }
+      lam = lam * P.beta;
+      if (nls > 64) {
+        status = 1;
+        break;
+      }
+      continue;
+    }
+    // ---- direct pass: K trial lambdas streamed over (x_tf, d_tf, gn)
     double lamk[K];
     lamk[0] = lam;
 #pragma unroll
@@ -423,77 +526,53 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
     double t[NT];
 #pragma unroll
     for (int k = 0; k < NT; ++k) t[k] = 0.0;
-    if (first) {
-      double t1[4] = {0.0, 0.0, 0.0, 0.0};  // lambda = 1 sums, const, dDiv/dbeta
-      const double l0 = lamk[0];
-      row_inv(G, B.spec, lds, [&](int r, int j, double v) {
-        const int i = r * G.W + j;
-        B.dtf[i] = v;
-        const double g = B.gns[i];
-        const double x0 = B.xtf[i];
-        const double bkv = bmap ? B.bks[i] : bks_scalar;
-        const double xt = x0 + l0 * v;
-        obj.terms(xt, xt + bkv, g, &t1[0]);
-        if (adapt) {
-          t1[2] += obj.konst(g);
-          t1[3] += beta_deriv_px(xt + bkv, g, obj.beta);
-        }
-      });
-      block_sum<4>(t1, red);
-      t[0] = t1[0];
-      t[1] = t1[1];
-      t[2 * K] = t1[2];
-      t[2 * K + 1] = t1[3];
-      first = false;
-    } else {
-      auto eval_px = [&](double x0, double dt, double g, double bkv) __attribute__((always_inline)) {
-        if (adapt) t[2 * K] += obj.konst(g);
+    auto eval_px = [&](double x0, double dt, double g, double bkv) __attribute__((always_inline)) {
+      if (adapt) t[2 * K] += obj.konst(g);
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const double xt = x0 + lamk[k] * dt;
-          const double den = xt + bkv;
-          obj.terms(xt, den, g, &t[2 * k]);
-        }
-        if (K == 1 && adapt) t[2 * K + 1] += beta_deriv_px(x0 + lamk[0] * dt + bkv, g, obj.beta);
-      };
-      const double* xtf = B.xtf;
-      const double* dtf = B.dtf;
-      const double* gns = B.gns;
-      const double* bks = B.bks;
-      stream2<1>(
-          npair,
-          [&](int p) {
-            struct V {
-              double2 x, d, g, b;
-            } v;
-            v.x = ld2(xtf, p);
-            v.d = ld2(dtf, p);
-            v.g = ld2(gns, p);
-            v.b = bmap ? ld2(bks, p) : double2{bks_scalar, bks_scalar};
-            return v;
-          },
-          [&](int p, const auto& v) {
-            eval_px(v.x.x, v.d.x, v.g.x, v.b.x);
-            if (!odd || 2 * p + 1 < N) eval_px(v.x.y, v.d.y, v.g.y, v.b.y);
-          });
-      block_sum<NT>(t, red);
-    }
+      for (int k = 0; k < K; ++k) {
+        const double xt = x0 + lamk[k] * dt;
+        const double den = xt + bkv;
+        obj.terms(xt, den, g, &t[2 * k]);
+      }
+      if (K == 1 && adapt) t[2 * K + 1] += beta_deriv_px(x0 + lamk[0] * dt + bkv, g, obj.beta);
+    };
+    const double* xtf = B.xtf;
+    const double* dtf = B.dtf;
+    const double* gns = B.gns;
+    const double* bks = B.bks;
+    stream2<1>(
+        npair,
+        [&](int p) {
+          struct V {
+            double2 x, d, g, b;
+          } v;
+          v.x = ld2(xtf, p);
+          v.d = ld2(dtf, p);
+          v.g = ld2(gns, p);
+          v.b = bmap ? ld2(bks, p) : double2{bks_scalar, bks_scalar};
+          return v;
+        },
+        [&](int p, const auto& v) {
+          eval_px(v.x.x, v.d.x, v.g.x, v.b.x);
+          if (!odd || 2 * p + 1 < N) eval_px(v.x.y, v.d.y, v.g.y, v.b.y);
+        });
+    block_sum<NT>(t, red);
     if (adapt) konst = t[2 * K];
     ++passes;
-    int acc = -1;
-    for (int k = 0; k < KK; ++k) {
-      if (acc < 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (!accepted) {
         const double fk = obj.combine(konst, t[2 * k], t[2 * k + 1], flux, (double)N);
         ++nls;
         if (fk <= fr + P.gamma * lamk[k] * gd || lamk[k] < 1e-12) {
-          acc = k;
+          accepted = true;
           f_acc = fk;
           lam = lamk[k];
         }
       }
     }
-    if (acc >= 0) break;
-    lam = lamk[KK - 1] * P.beta;
+    if (accepted) break;
+    lam = lamk[K - 1] * P.beta;
     if (adapt) {  // sgp.py:798-800: beta -= lr * mean(dDiv/dbeta)   (K == 1 here)
       const double bgrad = (obj.beta == 0.0 || obj.beta == 1.0) ? 0.0 : t[2 * K + 1] / N;
       obj.set_beta(obj.beta - st.lr * bgrad);
@@ -521,6 +600,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
     st.lam = lam_acc;
     st.E_ls += nls;
     st.ls_passes += passes;
+    st.ls_series += series_evals;
     st.status |= status;
   }
 }
@@ -642,11 +722,13 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
       A.out.iters[img] = it2 - 1;
       if (A.out.beta_final) A.out.beta_final[img] = st.beta;
       if (A.out.counters) {
-        int64_t* c = A.out.counters + (size_t)img * 4;
+        int64_t* c = A.out.counters + (size_t)img * 8;
         c[0] = st.E_p;
         c[1] = st.E_ls;
         c[2] = st.ls_passes;
         c[3] = st.status;
+        c[4] = st.ls_series;
+        c[5] = c[6] = c[7] = 0;
       }
       atomicSub(A.active, 1);
     }

@@ -75,7 +75,7 @@ typedef struct {
   int32_t schedule_lr;
   int32_t bkg_is_map;     /* bkg is [B][H][W] instead of [B] scalars               */
   int32_t ls_spec;        /* line-search lambdas evaluated per pass (1..8); 1 when adapt_beta */
-  int32_t reserved;
+  int32_t ls_series;      /* 1: small trial steps from the moment series (general beta) */
 } bsgp_params;
 
 /* Device inputs of a batched solve. */
@@ -96,8 +96,9 @@ typedef struct {
   double* crit;        /* [B][MAXIT1] stop-rule value per iteration, may be NULL  */
   int32_t* flags;      /* [B][MAXIT1] bit0: fv >= fr warning (sgp.py:351), may be NULL */
   double* beta_final;  /* [B] final betaParam (sgp.py:892), may be NULL           */
-  int64_t* counters;   /* [B][4]: proj evals E_p, line-search evals E_ls,
-                          line-search passes, status bits; may be NULL             */
+  int64_t* counters;   /* [B][8]: proj evals E_p, line-search trials E_ls,
+                          line-search passes over the image, status bits, trials
+                          evaluated from the small-step series, 3 reserved; may be NULL */
 } bsgp_outputs;
 
 /* Plan: geometry, FFT sizes, twiddles and the PSF transfer functions for A and

@@ -1,0 +1,29 @@
+// Host accuracy test of bsgp::fast_log (beta-sgp_amd/csrc/bsgp_math.hpp)
+// against long double log: max error in ulp over random normal inputs.
+#include <cmath>
+#include <cstdio>
+#include <random>
+#include "bsgp_math.hpp"
+
+int main() {
+  std::mt19937_64 rng(7);
+  double worst = 0, worst_x = 0;
+  auto check = [&](double x) {
+    long double ref = logl((long double)x);
+    double got = bsgp::fast_log(x);
+    double r = (double)ref;
+    double ulp = std::fabs(std::nextafter(r, INFINITY) - r);
+    if (r == 0) ulp = 4.9e-324;
+    double e = std::fabs((long double)got - ref) / ulp;
+    if (e > worst) { worst = e; worst_x = x; }
+  };
+  std::uniform_real_distribution<double> ue(-700, 700), uu(0.5, 2.0);
+  for (int i = 0; i < 2000000; ++i) check(std::exp(ue(rng)));
+  for (int i = 0; i < 2000000; ++i) check(uu(rng));
+  for (int i = 0; i < 200000; ++i) check(1.0 + (uu(rng) - 1.25) * 1e-6);
+  check(1.0); check(2.0); check(0.5); check(1e-300); check(1e300);
+  printf("fast_log max error %.3f ulp at x=%.17g\n", worst, worst_x);
+  bool ok = worst < 1.0 && std::isnan(bsgp::fast_log(-1.0)) && std::isinf(bsgp::fast_log(0.0));
+  printf(ok ? "math: all ok\n" : "math: FAIL\n");
+  return ok ? 0 : 1;
+}
