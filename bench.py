@@ -95,6 +95,25 @@ def cpu_baseline(n, k, nstars, images, maxit, workers):
                       f"({iters / cpu_s:.1f} image-it/s per core)"}
 
 
+def shard_seed0(rank, images_per_rank):
+    """Rank r solves images [r*B, (r+1)*B) of the synthetic stream: disjoint
+    shards, no data-path collective."""
+    return rank * images_per_rank
+
+
+def aggregate(dist, elapsed, iters_sum, device):
+    """Cross-rank reduction of one timed run: the max wall time over ranks and
+    the total image-iterations of all ranks (the only collectives of the
+    harness).  Works with any torch.distributed backend (nccl on the GPU box,
+    gloo in the CPU tests)."""
+    t = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
+    n = torch.tensor([float(iters_sum)], dtype=torch.float64, device=device)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(n.item())
+
+
 def load_traffic(config):
     f = os.path.join(ROOT, "profiles", f"traffic_{config}.json")
     if os.path.exists(f):
@@ -138,7 +157,7 @@ def main():
 
     n, k, nstars = 256, 25, 200
     B = args.batch if args.batch else (1024 if args.config == "c3" else 1)
-    gn, psf = synth_batch(B, n, k, nstars, seed0=rank * B)
+    gn, psf = synth_batch(B, n, k, nstars, seed0=shard_seed0(rank, B))
     bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
     kw = solve_kwargs(args.maxit, args.ls_spec)
     torch.cuda.synchronize()
@@ -169,13 +188,8 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     iters = out["iters"].cpu().numpy()
     cnt = out["counters"].cpu().numpy()
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    tot = torch.tensor([float(iters.sum())], dtype=torch.float64, device="cuda")
-    if dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    elapsed_max = float(t.item())
-    total_iters = float(tot.item()) * args.steps
+    elapsed_max, tot = aggregate(dist, elapsed, iters.sum(), "cuda")
+    total_iters = tot * args.steps
     value = total_iters / elapsed_max
 
     # algorithmic bytes per launch, b = 0 (scalar background)
