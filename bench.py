@@ -69,14 +69,14 @@ def synth_batch(B, n, k, nstars, seed0, bkg=100.0):
     return gn.contiguous(), psf
 
 
-def solve_kwargs(maxit, ls_spec):
+def solve_kwargs(maxit, ls_spec, streams=None):
     max_projs, gamma, beta, alpha_min, alpha_max, alpha, M_alpha, tau, M = (
         1000, 1e-4, 0.4, 1e-5, 1e5, 1e1, 3, 0.5, 1)  # sgp.DEFAULT_PARAMS (sgp.py:34)
     return dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=maxit, gamma=gamma, beta=beta,
                 alpha=alpha, alpha_min=alpha_min, alpha_max=alpha_max, M_alpha=M_alpha, tau=tau,
                 M=M, max_projs=max_projs, ccd_sat_level=65000.0, scale_data=True,
                 use_original_SGP_Afunction=False, adapt_beta=False, betaParam=1.05, lr=1e-3,
-                lr_exp_param=0.1, schedule_lr=True, ls_spec=ls_spec)
+                lr_exp_param=0.1, schedule_lr=True, ls_spec=ls_spec, streams=streams)
 
 
 def cpu_baseline(n, k, nstars, images, maxit, workers):
@@ -86,6 +86,7 @@ def cpu_baseline(n, k, nstars, images, maxit, workers):
     import cpu_bench
     kw = solve_kwargs(maxit, None)
     kw.pop("ls_spec")
+    kw.pop("streams")
     iters, wall, cpu_s = cpu_bench.run_pool(n, k, nstars, images, kw, workers)
     return {"value": iters / wall, "unit": "image-iterations/s", "cores": workers,
             "kind": "port",
@@ -133,6 +134,7 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--maxit", type=int, default=100)
     ap.add_argument("--ls-spec", type=int, default=None)
+    ap.add_argument("--streams", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-images", type=int, default=16)
     ap.add_argument("--cpu-maxit", type=int, default=20)
@@ -159,7 +161,7 @@ def main():
     B = args.batch if args.batch else (1024 if args.config == "c3" else 1)
     gn, psf = synth_batch(B, n, k, nstars, seed0=shard_seed0(rank, B))
     bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
-    kw = solve_kwargs(args.maxit, args.ls_spec)
+    kw = solve_kwargs(args.maxit, args.ls_spec, args.streams)
     torch.cuda.synchronize()
 
     def step():
@@ -217,14 +219,17 @@ def main():
                                f"MAXIT={args.maxit}, stop_criterion=1",
                    "images_per_gpu": B, "image": [n, n], "psf": [k, k], "maxit": args.maxit,
                    "parallelism": f"{world} independent shards (no collective)",
-                   "ls_spec": kw["ls_spec"] or sgp.LS_SPEC_DEFAULT},
+                   "ls_spec": kw["ls_spec"] or sgp.LS_SPEC_DEFAULT,
+                   "streams": kw["streams"] or sgp.STREAMS_DEFAULT},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic.get("bytes_per_launch") if traffic else None,
                      "kernel": "bsgp::sgp_solve_kernel", "kernel_ms": kern_ms,
                      "alg_bytes_per_launch": alg_bytes,
                      "E_p_per_iter": float(E_p.sum() / iters.sum()),
-                     "E_ls_per_iter": float(E_ls.sum() / iters.sum())},
+                     "E_ls_per_iter": float(E_ls.sum() / iters.sum()),
+                     "ls_passes_per_iter": float(cnt[:, 2].sum() / iters.sum()),
+                     "ls_series_per_iter": float(cnt[:, 4].sum() / iters.sum())},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -64,6 +64,12 @@ struct bsgp_plan_s {
   size_t st_n = 0;
   int* active = nullptr;     // device counter of images still iterating
   int* active_h = nullptr;   // pinned host mirror for polling
+  // sub-batch streams: phases of different sub-batches overlap on the device
+  static constexpr int kMaxStreams = 4;
+  hipStream_t sub[kMaxStreams] = {};
+  hipEvent_t ev_fork = nullptr;
+  hipEvent_t ev_join[kMaxStreams] = {};
+  int nsub = 0;
   // operator workspace
   cd* opws = nullptr;
   size_t opws_slots = 0;
@@ -272,6 +278,11 @@ int bsgp_plan_destroy(bsgp_plan p) {
   if (p->tw) (void)hipFree(p->tw);
   if (p->tf) (void)hipFree(p->tf);
   if (p->ws) (void)hipFree(p->ws);
+  for (int i = 0; i < p->nsub; ++i) {
+    if (p->sub[i]) (void)hipStreamDestroy(p->sub[i]);
+    if (p->ev_join[i]) (void)hipEventDestroy(p->ev_join[i]);
+  }
+  if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
   if (p->st) (void)hipFree(p->st);
   if (p->active) (void)hipFree(p->active);
   if (p->active_h) (void)hipHostFree(p->active_h);
@@ -323,6 +334,8 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   a.in = *in;
   a.out = *out;
   a.B = B;
+  a.img0 = 0;
+  a.nimg = B;
   a.st = p->st;
   a.active = p->active;
   a.ws = p->ws;
@@ -333,20 +346,51 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   const int K = (prm->adapt_beta && prm->variant == BSGP_VARIANT_BETA)
                     ? 1
                     : (prm->ls_spec <= 1 ? 1 : prm->ls_spec <= 2 ? 2 : prm->ls_spec <= 4 ? 4 : 8);
+  // Sub-batches on their own streams (fork/join with the caller's stream):
+  // while one sub-batch runs the compute-bound line search the other can
+  // stream its memory-bound phases.
+  int S = prm->streams < 1 ? 1 : prm->streams;
+  if (S > bsgp_plan_s::kMaxStreams) S = bsgp_plan_s::kMaxStreams;
+  if (S > B) S = B;
+  if (S > 1 && p->nsub < S) {
+    if (!p->ev_fork) HIP_TRY(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
+    for (int i = p->nsub; i < S; ++i) {
+      HIP_TRY(hipStreamCreateWithFlags(&p->sub[i], hipStreamNonBlocking));
+      HIP_TRY(hipEventCreateWithFlags(&p->ev_join[i], hipEventDisableTiming));
+    }
+    p->nsub = S;
+  }
   // device counter of running images: every setup block adds one, every
   // stopping image subtracts one (k_bb)
   HIP_TRY(hipMemsetAsync(p->active, 0, 16, s));
-  HIP_TRY(launch_setup(a, p->lds_bytes, s));
+  hipStream_t ss[bsgp_plan_s::kMaxStreams];
+  SolveArgs sa[bsgp_plan_s::kMaxStreams];
+  if (S > 1) HIP_TRY(hipEventRecord(p->ev_fork, s));
+  for (int j = 0; j < S; ++j) {
+    ss[j] = S > 1 ? p->sub[j] : s;
+    if (S > 1) HIP_TRY(hipStreamWaitEvent(ss[j], p->ev_fork, 0));
+    sa[j] = a;
+    sa[j].img0 = (int)((int64_t)B * j / S);
+    sa[j].nimg = (int)((int64_t)B * (j + 1) / S) - sa[j].img0;
+    HIP_TRY(launch_setup(sa[j], p->lds_bytes, ss[j]));
+  }
   // Fixed-length runs (stop_criterion 0/1) are launched back to back with no
   // host synchronisation; data-dependent stop rules poll the counter.
   const bool data_stop = prm->stop_criterion >= 2 && prm->stop_criterion <= 4;
   const int poll = data_stop ? (B <= 4 ? 1 : 4) : 0;
   for (int it = 1; it <= prm->MAXIT; ++it) {
-    HIP_TRY(launch_iteration(a, K, p->lds_bytes, s));
+    for (int j = 0; j < S; ++j) HIP_TRY(launch_iteration(sa[j], K, p->lds_bytes, ss[j]));
     if (poll && it < prm->MAXIT && it % poll == 0) {
-      HIP_TRY(hipMemcpyAsync(p->active_h, p->active, sizeof(int), hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipStreamSynchronize(s));
+      for (int j = 0; j < S; ++j) HIP_TRY(hipStreamSynchronize(ss[j]));
+      HIP_TRY(hipMemcpyAsync(p->active_h, p->active, sizeof(int), hipMemcpyDeviceToHost, ss[0]));
+      HIP_TRY(hipStreamSynchronize(ss[0]));
       if (*p->active_h <= 0) break;
+    }
+  }
+  if (S > 1) {
+    for (int j = 0; j < S; ++j) {
+      HIP_TRY(hipEventRecord(p->ev_join[j], ss[j]));
+      HIP_TRY(hipStreamWaitEvent(s, p->ev_join[j], 0));
     }
   }
   return BSGP_OK;

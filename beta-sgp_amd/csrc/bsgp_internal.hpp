@@ -28,6 +28,7 @@ struct SolveArgs {
   bsgp_inputs in;
   bsgp_outputs out;
   int B;
+  int img0, nimg;      // this launch's sub-batch [img0, img0 + nimg)
   ImgState* st;        // [B]
   int* active;         // images still iterating
   double* ws;          // per-image slots

@@ -136,7 +136,7 @@ __device__ __forceinline__ Objective make_obj(const SolveArgs& A, double beta) {
 // projection, x_tf = A(x), f, g and the scaling-matrix bounds.
 __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   BSGP_LDS_VIEWS(A);
-  const int img = blockIdx.x;
+  const int img = A.img0 + blockIdx.x;
   const Geo& G = A.g;
   const bsgp_params& P = A.prm;
   const int N = G.H * G.W;
@@ -306,7 +306,7 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
 // d.g, and the row transforms of d.
 __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
   BSGP_LDS_VIEWS(A);
-  const int img = blockIdx.x;
+  const int img = A.img0 + blockIdx.x;
   ImgState& st = A.st[img];
   if (st.stop) return;
   const Geo& G = A.g;
@@ -372,7 +372,7 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
 // ----------------------------------------------------------- kernel: columns
 __global__ void __launch_bounds__(kBlock) k_col(SolveArgs A, int transpose) {
   BSGP_LDS_VIEWS(A);
-  const int img = blockIdx.x;
+  const int img = A.img0 + blockIdx.x;
   if (A.st[img].stop) return;
   Bufs B = slot_bufs(A, img, 0);
   col_conv(A.g, B.spec, transpose ? A.g.tfAT : A.g.tfA, lds);
@@ -388,7 +388,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
   // which is where most non-stagnating iterations accept; later passes
   // stream K trial lambdas each.
   BSGP_LDS_VIEWS(A);
-  const int img = blockIdx.x;
+  const int img = A.img0 + blockIdx.x;
   ImgState& st = A.st[img];
   if (st.stop) return;
   const Geo& G = A.g;
@@ -611,7 +611,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
 // and the outputs once the image stops (sgp.py:424-438).
 __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
   BSGP_LDS_VIEWS(A);
-  const int img = blockIdx.x;
+  const int img = A.img0 + blockIdx.x;
   ImgState& st = A.st[img];
   if (st.stop) return;
   const Geo& G = A.g;
@@ -839,11 +839,11 @@ __global__ void grad_parts_kernel(int64_t n, const double* den, const double* gn
 
 // ----------------------------------------------------------- launchers
 hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL(k_setup, dim3(a.B), dim3(kBlock), lds, s, a);
+  hipLaunchKernelGGL(k_setup, dim3(a.nimg), dim3(kBlock), lds, s, a);
   return hipGetLastError();
 }
 hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
-  const dim3 grid(a.B), block(kBlock);
+  const dim3 grid(a.nimg), block(kBlock);
   hipLaunchKernelGGL(k_dir, grid, block, lds, s, a);
   hipLaunchKernelGGL(k_col, grid, block, lds, s, a, 0);
   switch (K) {

@@ -45,6 +45,7 @@ DEFAULT_COLUMNS = ['label', 'xcentroid', 'ycentroid', 'sky_centroid',
 
 LS_SPEC_DEFAULT = 2  # line-search trial lambdas evaluated per pass over the data
 LS_SERIES_DEFAULT = 1  # small line-search steps from the moment series (general beta)
+STREAMS_DEFAULT = 1  # sub-batch streams of a batched solve
 
 
 # ------------------------------------------------------------------ helpers
@@ -97,7 +98,7 @@ def _prelude_host(gn, bkg, init_recon, flux, stop_criterion, scale_data):
 def _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, alpha, alpha_min,
             alpha_max, M_alpha, tau, M, max_projs, verbose, ccd_sat_level, scale_data,
             tol_convergence, adapt_beta=False, betaParam=1.005, lr=1e-3, lr_exp_param=0.1,
-            schedule_lr=False, bkg_is_map=False, ls_spec=None, ls_series=None):
+            schedule_lr=False, bkg_is_map=False, ls_spec=None, ls_series=None, streams=None):
     p = _B.Params()
     p.variant = variant
     p.init_recon = int(init_recon)
@@ -121,6 +122,7 @@ def _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, 
     ls = LS_SPEC_DEFAULT if ls_spec is None else int(ls_spec)
     p.ls_spec = 1 if (variant == _B.BSGP_VARIANT_BETA and adapt_beta) else ls
     p.ls_series = LS_SERIES_DEFAULT if ls_series is None else int(bool(ls_series))
+    p.streams = STREAMS_DEFAULT if streams is None else int(streams)
     return p
 
 
@@ -292,7 +294,7 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
                  ccd_sat_level=None, scale_data=True, tol_convergence=1e-4,
                  use_original_SGP_Afunction=True, adapt_beta=False, betaParam=1.005, lr=1e-3,
                  lr_exp_param=0.1, schedule_lr=False, ls_spec=None, ls_series=None,
-                 device_out=False):
+                 streams=None, device_out=False):
     _check_psf(np.asarray(psf))
     torch = _B.torch
     _B.require_gpu()
@@ -309,7 +311,7 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
                   alpha_min, alpha_max, M_alpha, tau, M, max_projs, verbose, ccd_sat_level,
                   scale_data, tol_convergence, adapt_beta=adapt_beta, betaParam=betaParam, lr=lr,
                   lr_exp_param=lr_exp_param, schedule_lr=schedule_lr, bkg_is_map=bkg_is_map,
-                  ls_spec=ls_spec, ls_series=ls_series)
+                  ls_spec=ls_spec, ls_series=ls_series, streams=streams)
     x0 = None
     if init_recon == 1:
         np.random.seed(42)

@@ -76,6 +76,8 @@ typedef struct {
   int32_t bkg_is_map;     /* bkg is [B][H][W] instead of [B] scalars               */
   int32_t ls_spec;        /* line-search lambdas evaluated per pass (1..8); 1 when adapt_beta */
   int32_t ls_series;      /* 1: small trial steps from the moment series (general beta) */
+  int32_t streams;        /* sub-batches run on this many streams (1..4) so phases overlap */
+  int32_t reserved;
 } bsgp_params;
 
 /* Device inputs of a batched solve. */
