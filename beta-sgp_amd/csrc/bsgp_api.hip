@@ -262,7 +262,7 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   }
   const size_t N = (size_t)H * W;
   p->vec_stride = round_up(N, 32);
-  p->slot_stride = 8 * p->vec_stride + round_up((size_t)H * g.Qh * 2, 32);
+  p->slot_stride = 9 * p->vec_stride + round_up((size_t)H * g.Qh * 2, 32);
   if (hipMalloc(&p->active, 256) != hipSuccess ||
       hipHostMalloc(&p->active_h, 256, hipHostMallocDefault) != hipSuccess) {
     bsgp_plan_destroy(p);

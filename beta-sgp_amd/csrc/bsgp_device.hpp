@@ -503,6 +503,22 @@ struct Objective {
     if (mode == 3) return scal * fpow(gnv, beta);
     return 0.0;
   }
+  // lambda-dependent parts for one pixel with the mode fixed at compile time
+  // (MODE < 0: runtime mode)
+  template <int MODE>
+  __device__ __forceinline__ void terms_m(double xtf_try, double den, double gnv,
+                                         double* t) const {
+    if constexpr (MODE == 0) {
+      t[0] += gnv * fast_log(gnv / den);
+      t[1] += xtf_try;
+    } else if constexpr (MODE == 3) {
+      const double p = fpow(den, beta - 1);
+      t[0] += c1 * (den * p);
+      t[1] += (c2 * gnv) * p;
+    } else {
+      terms(xtf_try, den, gnv, t);
+    }
+  }
   // lambda-dependent parts for one pixel: adds to t[0..1]
   __device__ __forceinline__ void terms(double xtf_try, double den, double gnv, double* t) const {
     if (mode == 0) {

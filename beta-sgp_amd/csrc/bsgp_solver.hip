@@ -56,6 +56,8 @@ __device__ __forceinline__ double2 ld2(const double* a, int p) {
 // iterate).  Slot = image: state persists across the phase kernels.
 struct Bufs {
   double *gns, *bks, *xa, *xb, *ga, *gb, *xtf, *dtf;
+  double* pw;  // den^(beta-1) at the current x_tf (beta objective): reused by the
+               // gradient (k_bb) and the next line search's series moments
   cd* spec;
 };
 
@@ -75,7 +77,8 @@ __device__ __forceinline__ Bufs slot_bufs(const SolveArgs& A, int img, int par) 
   b.gb = par ? g0 : g1;
   b.xtf = ws + 6 * v;
   b.dtf = ws + 7 * v;
-  b.spec = reinterpret_cast<cd*>(ws + 8 * v);
+  b.pw = ws + 8 * v;
+  b.spec = reinterpret_cast<cd*>(ws + 9 * v);
   return b;
 }
 
@@ -226,6 +229,7 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   row_fwd(G, G.H, G.W, B.spec, lds, [&](int r, int j) { return B.xa[r * G.W + j]; });
   __syncthreads();
   col_conv(G, B.spec, G.tfA, lds);
+  const bool beta_obj = P.variant == BSGP_VARIANT_BETA;
   row_inv_fwd(G, B.spec, lds, [&](int r, int j, double v) {
     const int i = r * G.W + j;
     B.xtf[i] = v;
@@ -233,15 +237,17 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     const double g = B.gns[i];
     fsum[0] += obj.konst(g);
     obj.terms(v, den, g, &fsum[1]);
-    return obj.grad_w(den, g);
+    if (!beta_obj) return g / den;  // KL: w = gn/den (sgp.py:262)
+    const double p = fpow(den, obj.beta - 1);
+    B.pw[i] = p;
+    return g * (p / den);  // gn*den^(b-2) (sgp.py:499)
   });
   block_sum<3>(fsum, red);  // its barrier publishes xtf / spec
   const double fv = obj.combine(fsum[0], fsum[1], fsum[2], flux, (double)N);
   col_conv(G, B.spec, G.tfAT, lds);
   row_inv(G, B.spec, lds, [&](int r, int j, double at) {
     const int i = r * G.W + j;
-    const double den = B.xtf[i] + (bmap ? B.bks[i] : bks_scalar);
-    B.ga[i] = obj.grad_g1(den) - at;
+    B.ga[i] = (beta_obj ? B.pw[i] : 1.0) - at;  // sgp.py:263 / 499
   });
   __syncthreads();
   // scaling-matrix bounds from AT(gn) (sgp.py:268-273)
@@ -382,7 +388,7 @@ __global__ void __launch_bounds__(kBlock) k_col(SolveArgs A, int transpose) {
 // sgp.py:326-349 / 774-801: K trial lambdas per pass over (x_tf, d_tf, gn);
 // the first pass is fused into the inverse row transforms that produce d_tf.
 // Then x_tf += lam*d_tf and the row transforms of AT's input w.
-template <int K>
+template <int K, int MODE, bool ADAPT>
 __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
   // first pass (fused into the inverse rows of A(d)): one trial lambda = 1,
   // which is where most non-stagnating iterations accept; later passes
@@ -398,7 +404,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
   const bool odd = (N & 1) != 0;
   const int tid = threadIdx.x;
   const bool bmap = P.bkg_is_map != 0;
-  const bool adapt = P.adapt_beta && P.variant == BSGP_VARIANT_BETA;
+  constexpr bool adapt = ADAPT;  // adaptive beta (sgp.py:798-800): K == 1, runtime mode
   Bufs B = slot_bufs(A, img, st.par);
   const double bks_scalar = st.bks_scalar;
   const double flux = st.flux;
@@ -419,10 +425,10 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
   //   sum den^b        = sum_m binom(b, m)   lam^m P_m,  P_m = sum a^b u^m
   //   sum gn den^(b-1) = sum_m binom(b-1, m) lam^m Q_m,  Q_m = sum gn a^(b-1) u^m
   // so every trial with lam * max|u| <= kSeriesRho is evaluated without a pass
-  // over the image (truncation < 1e-17 relative at MS = 8).
-  constexpr int MS = 8;
+  // over the image (truncation < 1e-17 relative at MS = 6: (0.01)^7 * binom).
+  constexpr int MS = 6;
   constexpr double kSeriesRho = 0.01;
-  const bool series = P.ls_series != 0 && !adapt && obj.mode == 3;
+  const bool series = MODE == 3 && !adapt && P.ls_series != 0;
   double Pm[MS + 1], Qm[MS + 1];
   double rho = INFINITY;
   // ---- pass 1, fused into the inverse rows that produce d_tf: lam = 1 direct
@@ -439,15 +445,15 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
       const double x0 = B.xtf[i];
       const double bkv = bmap ? B.bks[i] : bks_scalar;
       const double xt = x0 + lam * v;
-      obj.terms(xt, xt + bkv, g, &t1[0]);
-      if (adapt) {
+      obj.template terms_m<MODE>(xt, xt + bkv, g, &t1[0]);
+      if constexpr (adapt) {
         t1[2] += obj.konst(g);
         t1[3] += beta_deriv_px(xt + bkv, g, obj.beta);
       }
       if (series) {
         const double a = x0 + bkv;
         const double u = v / a;
-        const double p0 = fpow(a, obj.beta - 1);
+        const double p0 = B.pw[i];  // = fpow(a, beta-1), stored at the last accept
         const double A0 = a * p0, B0 = g * p0;
         double um = 1.0;
 #pragma unroll
@@ -527,14 +533,15 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
 #pragma unroll
     for (int k = 0; k < NT; ++k) t[k] = 0.0;
     auto eval_px = [&](double x0, double dt, double g, double bkv) __attribute__((always_inline)) {
-      if (adapt) t[2 * K] += obj.konst(g);
+      if constexpr (adapt) t[2 * K] += obj.konst(g);
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const double xt = x0 + lamk[k] * dt;
         const double den = xt + bkv;
-        obj.terms(xt, den, g, &t[2 * k]);
+        obj.template terms_m<MODE>(xt, den, g, &t[2 * k]);
       }
-      if (K == 1 && adapt) t[2 * K + 1] += beta_deriv_px(x0 + lamk[0] * dt + bkv, g, obj.beta);
+      if constexpr (K == 1 && adapt)
+        t[2 * K + 1] += beta_deriv_px(x0 + lamk[0] * dt + bkv, g, obj.beta);
     };
     const double* xtf = B.xtf;
     const double* dtf = B.dtf;
@@ -589,7 +596,11 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
     const double xt = B.xtf[i] + lam_acc * B.dtf[i];
     B.xtf[i] = xt;
     const double den = xt + (bmap ? B.bks[i] : bks_scalar);
-    return obj.grad_w(den, B.gns[i]);
+    const double g = B.gns[i];
+    if (P.variant != BSGP_VARIANT_BETA) return g / den;  // KL: w = gn/den
+    const double p = fpow(den, obj.beta - 1);
+    B.pw[i] = p;
+    return g * (p / den);
   });
   if (tid == 0) {
     if (A.out.flags)
@@ -619,6 +630,7 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
   const int N = G.H * G.W;
   const int tid = threadIdx.x;
   const bool bmap = P.bkg_is_map != 0;
+  const bool beta_obj = P.variant == BSGP_VARIANT_BETA;
   Bufs B = slot_bufs(A, img, st.par);
   Dir D = make_dir(A, st);
   const double lam = st.lam;
@@ -628,8 +640,7 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
   double bb[6] = {0, 0, 0, 0, 0, 0};  // bk, ck, sk2.sk2, yk2.yk2, sk.sk, x.x
   row_inv(G, B.spec, lds, [&](int r, int j, double at) {
     const int i = r * G.W + j;
-    const double den = B.xtf[i] + (bmap ? B.bks[i] : bks_scalar);
-    const double gnew = obj.grad_g1(den) - at;
+    const double gnew = (beta_obj ? B.pw[i] : 1.0) - at;  // sgp.py:342 / 790
     const double x = B.xa[i], g = B.ga[i];
     const double d = D.d(x, g);
     const double sk = lam * d;
@@ -846,11 +857,30 @@ hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s
   const dim3 grid(a.nimg), block(kBlock);
   hipLaunchKernelGGL(k_dir, grid, block, lds, s, a);
   hipLaunchKernelGGL(k_col, grid, block, lds, s, a, 0);
-  switch (K) {
-    case 1: hipLaunchKernelGGL(k_ls<1>, grid, block, lds, s, a); break;
-    case 2: hipLaunchKernelGGL(k_ls<2>, grid, block, lds, s, a); break;
-    case 4: hipLaunchKernelGGL(k_ls<4>, grid, block, lds, s, a); break;
-    default: hipLaunchKernelGGL(k_ls<8>, grid, block, lds, s, a); break;
+  // line-search kernel specialised on trial width, objective mode, adaptivity
+  const bsgp_params& P = a.prm;
+  const bool adapt = P.adapt_beta && P.variant == BSGP_VARIANT_BETA;
+  const int mode = P.variant == BSGP_VARIANT_KL ? 0
+                   : (P.betaParam == 0.0 || P.betaParam == 1.0 || a.in.beta0) ? -1
+                                                                                : 3;
+  if (adapt) {
+    hipLaunchKernelGGL((k_ls<1, -1, true>), grid, block, lds, s, a);
+  } else if (mode == 0) {
+    switch (K) {
+      case 1: hipLaunchKernelGGL((k_ls<1, 0, false>), grid, block, lds, s, a); break;
+      case 2: hipLaunchKernelGGL((k_ls<2, 0, false>), grid, block, lds, s, a); break;
+      case 4: hipLaunchKernelGGL((k_ls<4, 0, false>), grid, block, lds, s, a); break;
+      default: hipLaunchKernelGGL((k_ls<8, 0, false>), grid, block, lds, s, a); break;
+    }
+  } else if (mode == 3) {
+    switch (K) {
+      case 1: hipLaunchKernelGGL((k_ls<1, 3, false>), grid, block, lds, s, a); break;
+      case 2: hipLaunchKernelGGL((k_ls<2, 3, false>), grid, block, lds, s, a); break;
+      case 4: hipLaunchKernelGGL((k_ls<4, 3, false>), grid, block, lds, s, a); break;
+      default: hipLaunchKernelGGL((k_ls<8, 3, false>), grid, block, lds, s, a); break;
+    }
+  } else {
+    hipLaunchKernelGGL((k_ls<2, -1, false>), grid, block, lds, s, a);
   }
   hipLaunchKernelGGL(k_col, grid, block, lds, s, a, 1);
   hipLaunchKernelGGL(k_bb, grid, block, lds, s, a);
@@ -895,9 +925,21 @@ hipError_t launch_grad_parts(int64_t n, const double* den, const double* gn, dou
   return hipGetLastError();
 }
 hipError_t set_solver_lds_limit(size_t bytes) {
-  const void* fns[] = {(const void*)k_setup,     (const void*)k_dir,       (const void*)k_col,
-                       (const void*)k_ls<1>,     (const void*)k_ls<2>,     (const void*)k_ls<4>,
-                       (const void*)k_ls<8>,     (const void*)k_bb,        (const void*)apply_op_kernel,
+  const void* fns[] = {(const void*)k_setup,
+                       (const void*)k_dir,
+                       (const void*)k_col,
+                       (const void*)k_ls<1, -1, true>,
+                       (const void*)k_ls<1, 0, false>,
+                       (const void*)k_ls<2, 0, false>,
+                       (const void*)k_ls<4, 0, false>,
+                       (const void*)k_ls<8, 0, false>,
+                       (const void*)k_ls<1, 3, false>,
+                       (const void*)k_ls<2, 3, false>,
+                       (const void*)k_ls<4, 3, false>,
+                       (const void*)k_ls<8, 3, false>,
+                       (const void*)k_ls<2, -1, false>,
+                       (const void*)k_bb,
+                       (const void*)apply_op_kernel,
                        (const void*)build_tf_kernel};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);

@@ -45,7 +45,7 @@ DEFAULT_COLUMNS = ['label', 'xcentroid', 'ycentroid', 'sky_centroid',
 
 LS_SPEC_DEFAULT = 2  # line-search trial lambdas evaluated per pass over the data
 LS_SERIES_DEFAULT = 1  # small line-search steps from the moment series (general beta)
-STREAMS_DEFAULT = 1  # sub-batch streams of a batched solve
+STREAMS_DEFAULT = 2  # sub-batch streams of a batched solve
 
 
 # ------------------------------------------------------------------ helpers
