@@ -69,14 +69,15 @@ def synth_batch(B, n, k, nstars, seed0, bkg=100.0):
     return gn.contiguous(), psf
 
 
-def solve_kwargs(maxit, ls_spec, streams=None):
+def solve_kwargs(maxit, ls_spec, streams=None, team=None):
     max_projs, gamma, beta, alpha_min, alpha_max, alpha, M_alpha, tau, M = (
         1000, 1e-4, 0.4, 1e-5, 1e5, 1e1, 3, 0.5, 1)  # sgp.DEFAULT_PARAMS (sgp.py:34)
     return dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=maxit, gamma=gamma, beta=beta,
                 alpha=alpha, alpha_min=alpha_min, alpha_max=alpha_max, M_alpha=M_alpha, tau=tau,
                 M=M, max_projs=max_projs, ccd_sat_level=65000.0, scale_data=True,
                 use_original_SGP_Afunction=False, adapt_beta=False, betaParam=1.05, lr=1e-3,
-                lr_exp_param=0.1, schedule_lr=True, ls_spec=ls_spec, streams=streams)
+                lr_exp_param=0.1, schedule_lr=True, ls_spec=ls_spec, streams=streams,
+                team=team)
 
 
 def cpu_baseline(n, k, nstars, images, maxit, workers):
@@ -135,6 +136,8 @@ def main():
     ap.add_argument("--maxit", type=int, default=100)
     ap.add_argument("--ls-spec", type=int, default=None)
     ap.add_argument("--streams", type=int, default=None)
+    ap.add_argument("--team", type=int, default=None,
+                    help="workgroups per image (0/None = auto, 1 = one per image)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-images", type=int, default=16)
     ap.add_argument("--cpu-maxit", type=int, default=20)
@@ -161,7 +164,7 @@ def main():
     B = args.batch if args.batch else (1024 if args.config == "c3" else 1)
     gn, psf = synth_batch(B, n, k, nstars, seed0=shard_seed0(rank, B))
     bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
-    kw = solve_kwargs(args.maxit, args.ls_spec, args.streams)
+    kw = solve_kwargs(args.maxit, args.ls_spec, args.streams, args.team)
     torch.cuda.synchronize()
 
     def step():
@@ -220,7 +223,8 @@ def main():
                    "images_per_gpu": B, "image": [n, n], "psf": [k, k], "maxit": args.maxit,
                    "parallelism": f"{world} independent shards (no collective)",
                    "ls_spec": kw["ls_spec"] or sgp.LS_SPEC_DEFAULT,
-                   "streams": kw["streams"] or sgp.STREAMS_DEFAULT},
+                   "streams": kw["streams"] or sgp.STREAMS_DEFAULT,
+                   "team": int(cnt[0, 5])},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic.get("bytes_per_launch") if traffic else None,

@@ -51,7 +51,7 @@ class Params(ctypes.Structure):
         ("has_sat", ctypes.c_int32), ("scale_data", ctypes.c_int32), ("verbose", ctypes.c_int32),
         ("adapt_beta", ctypes.c_int32), ("schedule_lr", ctypes.c_int32),
         ("bkg_is_map", ctypes.c_int32), ("ls_spec", ctypes.c_int32), ("ls_series", ctypes.c_int32),
-        ("streams", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("streams", ctypes.c_int32), ("team", ctypes.c_int32),
     ]
 
 
@@ -199,6 +199,17 @@ class Plan:
         check(lib().bsgp_solve_device(self.h, B, ctypes.byref(params), ctypes.byref(ins),
                                       ctypes.byref(outs), current_stream()))
         return out
+
+
+STATUS_TEAM_TIMEOUT = 4
+
+
+def check_status(counters):
+    """Raise if a solve reported a team-barrier timeout (counters[:, 3] bit 4):
+    its results are not valid."""
+    st = counters[:, 3].cpu().numpy()
+    if np.any(st & STATUS_TEAM_TIMEOUT):
+        raise BsgpError(BSGP_ERR_HIP, "team barrier timed out (workgroups not co-resident)")
 
 
 _plan_cache = {}

@@ -70,6 +70,11 @@ struct bsgp_plan_s {
   hipEvent_t ev_fork = nullptr;
   hipEvent_t ev_join[kMaxStreams] = {};
   int nsub = 0;
+  // teams: reduction partials and barrier counters (+ the timeout word)
+  double* tpart = nullptr;
+  size_t tpart_n = 0;
+  unsigned int* tctr = nullptr;
+  size_t tctr_bytes = 0;
   // operator workspace
   cd* opws = nullptr;
   size_t opws_slots = 0;
@@ -89,6 +94,41 @@ static int ensure_ws(bsgp_plan p, size_t slots) {
     p->st_n = 0;
     HIP_TRY(hipMalloc(&p->st, slots * sizeof(ImgState)));
     p->st_n = slots;
+  }
+  return BSGP_OK;
+}
+
+// Workgroups per image.  Every member of every team must be resident at once
+// (the team barriers spin), so B*T <= CUs: one workgroup per CU always fits.
+// Each member keeps at least one row pair and one column per FFT wave.
+static int choose_team(const bsgp_plan_s* p, int B, int req) {
+  if (req == 1) return 1;
+  const Geo& g = p->g;
+  const int rows2 = (g.H + 1) / 2;
+  int tgeo = rows2 / g.nfw;
+  if (g.Qh / g.nfw < tgeo) tgeo = g.Qh / g.nfw;
+  int cap = p->ncu / B;
+  int T = cap < tgeo ? cap : tgeo;
+  if (req > 1 && req < T) T = req;
+  return T < 1 ? 1 : T;
+}
+
+static int ensure_team(bsgp_plan p, size_t B, int T) {
+  const size_t np = B * 2 * (size_t)T * kMaxRed;
+  if (T > 1 && np > p->tpart_n) {
+    if (p->tpart) HIP_TRY(hipFree(p->tpart));
+    p->tpart = nullptr;
+    p->tpart_n = 0;
+    HIP_TRY(hipMalloc(&p->tpart, np * sizeof(double)));
+    p->tpart_n = np;
+  }
+  const size_t cb = round_up((B + 1) * sizeof(unsigned int), 16);
+  if (cb > p->tctr_bytes) {
+    if (p->tctr) HIP_TRY(hipFree(p->tctr));
+    p->tctr = nullptr;
+    p->tctr_bytes = 0;
+    HIP_TRY(hipMalloc(&p->tctr, cb));
+    p->tctr_bytes = cb;
   }
   return BSGP_OK;
 }
@@ -287,6 +327,8 @@ int bsgp_plan_destroy(bsgp_plan p) {
   if (p->active) (void)hipFree(p->active);
   if (p->active_h) (void)hipHostFree(p->active_h);
   if (p->opws) (void)hipFree(p->opws);
+  if (p->tpart) (void)hipFree(p->tpart);
+  if (p->tctr) (void)hipFree(p->tctr);
   delete p;
   return BSGP_OK;
 }
@@ -328,6 +370,9 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   HIP_TRY(hipSetDevice(p->device));
   rc = ensure_ws(p, (size_t)B);
   if (rc) return rc;
+  const int T = choose_team(p, B, prm->team);
+  rc = ensure_team(p, (size_t)B, T);
+  if (rc) return rc;
   SolveArgs a;
   a.g = p->g;
   a.prm = *prm;
@@ -342,6 +387,10 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   a.slot_stride = p->slot_stride;
   a.vec_stride = p->vec_stride;
   a.lds_fft_bytes = p->lds_fft_bytes;
+  a.T = T;
+  a.tpart = T > 1 ? p->tpart : nullptr;
+  a.tctr = p->tctr;
+  a.tfail = reinterpret_cast<int*>(p->tctr + B);
   hipStream_t s = (hipStream_t)stream;
   const int K = (prm->adapt_beta && prm->variant == BSGP_VARIANT_BETA)
                     ? 1
@@ -363,6 +412,8 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   // device counter of running images: every setup block adds one, every
   // stopping image subtracts one (k_bb)
   HIP_TRY(hipMemsetAsync(p->active, 0, 16, s));
+  // team barrier counters and the timeout word restart at 0 every solve
+  HIP_TRY(hipMemsetAsync(p->tctr, 0, p->tctr_bytes, s));
   hipStream_t ss[bsgp_plan_s::kMaxStreams];
   SolveArgs sa[bsgp_plan_s::kMaxStreams];
   if (S > 1) HIP_TRY(hipEventRecord(p->ev_fork, s));

@@ -132,6 +132,135 @@ __device__ __forceinline__ double block_min(double v, double* red) {
   return s;
 }
 
+// --------------------------------------------------------------- teams
+// A team = T workgroups cooperating on one image (T = 1: one workgroup, no
+// global traffic).  Work is strided over the team's waves / threads; every
+// reduction is a team reduction: block totals -> per-member partials in
+// global memory -> team barrier -> fixed-order sum of the T partials, so all
+// members hold bit-identical scalars and run the same control flow.
+struct Team {
+  int m, T;            // member index, team size
+  double* part;        // [2][T][kMaxRed] partial slots of this image (double-buffered)
+  unsigned int* ctr;   // arrival counter of this image (monotonic across kernels)
+  unsigned int base;   // counter value when this kernel started (same in all members)
+  int nb;              // team barriers passed in this kernel
+  int* fail;           // set when a barrier spin times out (solve status bit 2)
+};
+
+// Work partition of a team: waves (rows / columns) and threads (pixel streams).
+struct Part {
+  int gw0, gws;  // first global wave index of this workgroup, global wave stride
+  int gt0, gts;  // first global thread index, global thread stride
+};
+
+__device__ __forceinline__ Part make_part(const Team& t, int nfw) {
+  Part d;
+  d.gw0 = t.m * nfw;
+  d.gws = t.T * nfw;
+  d.gt0 = t.m * kBlock;
+  d.gts = t.T * kBlock;
+  return d;
+}
+
+__device__ __forceinline__ Part solo_part(int nfw) {
+  Part d;
+  d.gw0 = 0;
+  d.gws = nfw;
+  d.gt0 = 0;
+  d.gts = kBlock;
+  return d;
+}
+
+// Team barrier with agent-scope release/acquire (cdna_hip_programming.md §6
+// Guideline 16): every storing wave drains its stores, the workgroup syncs,
+// lane 0 releases, arrives on the counter, polls it relaxed with s_sleep, and
+// acquires; the spin is bounded (timeout sets *fail and lets the kernel end).
+__device__ __forceinline__ void team_barrier(Team& t) {
+  if (t.T == 1) {
+    __syncthreads();
+    return;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(t.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int target = t.base + (unsigned int)(t.nb + 1) * (unsigned int)t.T;
+    unsigned int spins = 0;
+    while ((int)(__hip_atomic_load(t.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) <
+           0) {
+      __builtin_amdgcn_s_sleep(2);
+      ++spins;
+      // once any barrier of the solve timed out, every later one returns at
+      // once: the solve ends quickly with status bit 4 instead of hanging
+      if ((spins & 1023u) == 0 &&
+          __hip_atomic_load(t.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+        break;
+      if (spins > (1u << 24)) {
+        __hip_atomic_store(t.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  t.nb += 1;
+}
+
+// Team sum of NV values: every thread of every member gets the totals.
+template <int NV>
+__device__ __forceinline__ void team_sum(double (&v)[NV], double* red, Team& t) {
+  block_sum<NV>(v, red);
+  if (t.T == 1) return;
+  double* slot = t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) slot[(size_t)t.m * kMaxRed + i] = v[i];
+  }
+  team_barrier(t);
+  // thread i < NV adds partial i of all members in member order
+  if (threadIdx.x < NV) {
+    const int i = threadIdx.x;
+    double s = 0.0;
+    for (int mm = 0; mm < t.T; ++mm) s += slot[(size_t)mm * kMaxRed + i];
+    red[kWaves * kMaxRed + i] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = red[kWaves * kMaxRed + i];
+  __syncthreads();
+}
+
+// Team max / min (NaN propagates, like np.max / np.min)
+template <bool MAX>
+__device__ __forceinline__ double team_ext(double v, double* red, Team& t) {
+  v = MAX ? block_max(v, red) : block_min(v, red);
+  if (t.T == 1) return v;
+  double* slot = t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
+  if (threadIdx.x == 0) slot[(size_t)t.m * kMaxRed] = v;
+  team_barrier(t);
+  if (threadIdx.x == 0) {
+    double s = slot[0];
+    for (int mm = 1; mm < t.T; ++mm) {
+      const double u = slot[(size_t)mm * kMaxRed];
+      s = MAX ? ((u > s || u != u) ? u : s) : ((u < s || u != u) ? u : s);
+    }
+    red[kWaves * kMaxRed] = s;
+  }
+  __syncthreads();
+  const double r = red[kWaves * kMaxRed];
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ double team_max(double v, double* red, Team& t) {
+  return team_ext<true>(v, red, t);
+}
+__device__ __forceinline__ double team_min(double v, double* red, Team& t) {
+  return team_ext<false>(v, red, t);
+}
+
 // x**a for the divergence terms: exp(a*fast_log(x)) (bsgp_math.hpp).  For the
 // exponents of this path (|a| = |beta-1| <~ 1, scaled data so |log x| <~ 20)
 // the error is a few ulp at most, at ~1/2.6 the cost of the general pow();
@@ -150,19 +279,41 @@ __device__ __forceinline__ double py_max2(double a, double b) { return (b > a) ?
 __device__ __forceinline__ double py_min2(double a, double b) { return (b < a) ? b : a; }
 
 // --------------------------------------------------------------- conv passes
-// Spectrum scratch of one image: `nrows` rows x Qh complex, row-major.
-//
+// Spectrum scratch of one image is COLUMN-major: spec[k * ld + p] for stored
+// column k < Qh and row p < ld (ld = H: the zero-filled rows H..P-1 of the
+// padded grid are never stored).  A column is contiguous, so the column pass
+// streams it with coalesced 16-B loads straight into one wave's LDS buffer;
+// the row passes write/read (r, r+1) pairs, 32 contiguous bytes per column,
+// which the L2 merges across the workgroup's waves (rows 2w.. of wave w).
+struct alignas(32) CPair {
+  cd a, b;
+};
+
+__device__ __forceinline__ void store_pair(cd* col, bool two, bool pair_ok, cd ak, cd bk) {
+  if (two && pair_ok) {
+    CPair v;
+    v.a = ak;
+    v.b = bk;
+    *reinterpret_cast<CPair*>(col) = v;
+  } else {
+    col[0] = ak;
+    if (two) col[1] = bk;
+  }
+}
+
 // row_fwd: for every pair of image rows (r, r+1) one wave FFTs z = a + i b
-// (a, b real rows of length W zero-padded to Q) and stores the two half
-// spectra.  `prod(r, j)` produces the real input pixel (fused producer).
+// (a, b real rows of length ncols zero-padded to Q) and stores the two half
+// spectra into column-major spec with leading dimension ld (>= nrows).
+// `prod(r, j)` produces the real input pixel (fused producer).
 template <class Prod>
-__device__ __forceinline__ void row_fwd(const Geo& G, int nrows, int ncols, cd* spec, cd* lds,
-                                        Prod&& prod) {
+__device__ __forceinline__ void row_fwd(const Geo& G, const Part& D, int nrows, int ncols, int ld,
+                                        cd* spec, cd* lds, Prod&& prod) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool pair_ok = (ld & 1) == 0;
   if (w < G.nfw) {
     cd* a = lds + w * 2 * G.lpad;
     cd* b = a + G.lpad;
-    for (int r = 2 * w; r < nrows; r += 2 * G.nfw) {
+    for (int r = 2 * (D.gw0 + w); r < nrows; r += 2 * D.gws) {
       const bool two = (r + 1) < nrows;
       for (int j = lane; j < G.Q; j += 64) {
         double va = 0.0, vb = 0.0;
@@ -173,46 +324,43 @@ __device__ __forceinline__ void row_fwd(const Geo& G, int nrows, int ncols, cd* 
         a[j] = cmk(va, vb);
       }
       wave_sync();
-      cd* Z = fft_run(a, b, G.fq, false, lane, 64, WaveSync());
-      cd* A = spec + (size_t)r * G.Qh;
+      cd* Z = fft_any(a, b, G.fq, false, lane, 64, WaveSync());
       for (int k = lane; k < G.Qh; k += 64) {
         cd ak, bk;
         r2c_split(Z, G.Q, k, &ak, &bk);
-        A[k] = ak;
-        if (two) A[G.Qh + k] = bk;
+        store_pair(spec + (size_t)k * ld + r, two, pair_ok, ak, bk);
       }
       wave_sync();
     }
   }
 }
 
-// Rebuild the full-length row pair spectrum into `a` from stored half spectra.
-__device__ __forceinline__ void gather_pair(const Geo& G, const cd* A, bool two, cd* a, int lane) {
+// Rebuild the full-length spectrum of row pair (r, r+1) into `a`.
+__device__ __forceinline__ void gather_pair(const Geo& G, const cd* spec, int ld, int r, bool two,
+                                            cd* a, int lane) {
   for (int k = lane; k < G.Q; k += 64) {
-    cd z;
-    if (two) {
-      z = c2r_gather(A, A + G.Qh, G.Q, G.Qh, k);
-    } else {
-      const cd v = (k < G.Qh) ? A[k] : cconj(A[G.Q - k]);
-      z = v;
-    }
-    a[k] = z;
+    const bool lo = k < G.Qh;
+    const cd* col = spec + (size_t)(lo ? k : G.Q - k) * ld + r;
+    const cd A = col[0];
+    const cd B = two ? col[1] : cmk(0.0, 0.0);
+    a[k] = lo ? cmk(A.x - B.y, A.y + B.x) : cmk(A.x + B.y, B.x - A.y);
   }
 }
 
 // row_inv: inverse row transforms; `cons(r, j, value)` consumes each output
 // pixel (j < W) of rows [0, H).  The 1/(P*Q) scale is folded into the TF.
 template <class Cons>
-__device__ __forceinline__ void row_inv(const Geo& G, const cd* spec, cd* lds, Cons&& cons) {
+__device__ __forceinline__ void row_inv(const Geo& G, const Part& D, const cd* spec, cd* lds,
+                                        Cons&& cons) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (w < G.nfw) {
     cd* a = lds + w * 2 * G.lpad;
     cd* b = a + G.lpad;
-    for (int r = 2 * w; r < G.H; r += 2 * G.nfw) {
+    for (int r = 2 * (D.gw0 + w); r < G.H; r += 2 * D.gws) {
       const bool two = (r + 1) < G.H;
-      gather_pair(G, spec + (size_t)r * G.Qh, two, a, lane);
+      gather_pair(G, spec, G.H, r, two, a, lane);
       wave_sync();
-      cd* Z = fft_run(a, b, G.fq, true, lane, 64, WaveSync());
+      cd* Z = fft_any(a, b, G.fq, true, lane, 64, WaveSync());
 #pragma unroll 1
       for (int j = lane; j < G.W; j += 64) {
         const cd z = Z[j];
@@ -226,20 +374,21 @@ __device__ __forceinline__ void row_inv(const Geo& G, const cd* spec, cd* lds, C
 
 // row_inv_fwd: inverse rows of one convolution, then (same rows, same wave)
 // forward rows of the next one: `cp(r, j, value)` consumes the output pixel
-// and returns the next convolution's input pixel.  Spectrum rows are updated
-// in place.
+// and returns the next convolution's input pixel.  The spectrum is updated in
+// place (only this wave touches rows r, r+1).
 template <class CP>
-__device__ __forceinline__ void row_inv_fwd(const Geo& G, cd* spec, cd* lds, CP&& cp) {
+__device__ __forceinline__ void row_inv_fwd(const Geo& G, const Part& D, cd* spec, cd* lds,
+                                            CP&& cp) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool pair_ok = (G.H & 1) == 0;
   if (w < G.nfw) {
     cd* a = lds + w * 2 * G.lpad;
     cd* b = a + G.lpad;
-    for (int r = 2 * w; r < G.H; r += 2 * G.nfw) {
+    for (int r = 2 * (D.gw0 + w); r < G.H; r += 2 * D.gws) {
       const bool two = (r + 1) < G.H;
-      cd* A = spec + (size_t)r * G.Qh;
-      gather_pair(G, A, two, a, lane);
+      gather_pair(G, spec, G.H, r, two, a, lane);
       wave_sync();
-      cd* Z = fft_run(a, b, G.fq, true, lane, 64, WaveSync());
+      cd* Z = fft_any(a, b, G.fq, true, lane, 64, WaveSync());
       cd* in2 = (Z == a) ? b : a;
       for (int j = lane; j < G.Q; j += 64) {
         double va = 0.0, vb = 0.0;
@@ -251,55 +400,41 @@ __device__ __forceinline__ void row_inv_fwd(const Geo& G, cd* spec, cd* lds, CP&
         in2[j] = cmk(va, vb);
       }
       wave_sync();
-      cd* Y = fft_run(in2, Z, G.fq, false, lane, 64, WaveSync());
+      cd* Y = fft_any(in2, Z, G.fq, false, lane, 64, WaveSync());
       for (int k = lane; k < G.Qh; k += 64) {
         cd ak, bk;
         r2c_split(Y, G.Q, k, &ak, &bk);
-        A[k] = ak;
-        if (two) A[G.Qh + k] = bk;
+        store_pair(spec + (size_t)k * G.H + r, two, pair_ok, ak, bk);
       }
       wave_sync();
     }
   }
 }
 
-// col_conv: for every stored column k of the half spectrum, forward FFT over
-// the P-point column (rows >= H are the zero fill), multiply by tf[k][:],
-// inverse FFT, keep rows [0, H).  Columns are staged through LDS in tiles of
-// nfw columns with coalesced row-segment loads.
-__device__ __forceinline__ void col_conv(const Geo& G, cd* spec, const cd* tf, cd* lds) {
+// col_conv: every wave owns whole columns: it streams stored column k
+// (contiguous, H rows) into its LDS buffer, zero-fills rows H..P-1, runs the
+// forward P-point FFT, multiplies by tf[k][:], runs the inverse FFT and
+// writes rows [0, H) back.  No workgroup barrier inside the pass.
+__device__ __forceinline__ void col_conv(const Geo& G, const Part& D, cd* spec, const cd* tf,
+                                         cd* lds) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int C = G.nfw;
-  const int stride = 2 * G.lpad;
-  for (int k0 = 0; k0 < G.Qh; k0 += C) {
-    for (int idx = threadIdx.x; idx < G.P * C; idx += kBlock) {
-      const int p = idx / C, c = idx - p * C, k = k0 + c;
-      cd v = cmk(0.0, 0.0);
-      if (p < G.H && k < G.Qh) v = spec[(size_t)p * G.Qh + k];
-      lds[c * stride + p] = v;
-    }
-    __syncthreads();
-    if (w < C && k0 + w < G.Qh) {
-      cd* a = lds + w * stride;
-      cd* b = a + G.lpad;
-      cd* Z = fft_run(a, b, G.fp, false, lane, 64, WaveSync());
-      const cd* t = tf + (size_t)(k0 + w) * G.P;
+  if (w < G.nfw) {
+    cd* a = lds + w * 2 * G.lpad;
+    cd* b = a + G.lpad;
+    for (int k = D.gw0 + w; k < G.Qh; k += D.gws) {
+      cd* col = spec + (size_t)k * G.H;
+      for (int p = lane; p < G.P; p += 64) a[p] = (p < G.H) ? col[p] : cmk(0.0, 0.0);
+      wave_sync();
+      cd* Z = fft_any(a, b, G.fp, false, lane, 64, WaveSync());
+      const cd* t = tf + (size_t)k * G.P;
       for (int p = lane; p < G.P; p += 64) Z[p] = cmul(Z[p], t[p]);
       wave_sync();
-      cd* other = (Z == a) ? b : a;
-      cd* Y = fft_run(Z, other, G.fp, true, lane, 64, WaveSync());
-      if (Y != a) {
-        for (int p = lane; p < G.H; p += 64) a[p] = Y[p];
-        wave_sync();
-      }
+      cd* Y = fft_any(Z, (Z == a) ? b : a, G.fp, true, lane, 64, WaveSync());
+      for (int p = lane; p < G.H; p += 64) col[p] = Y[p];
+      wave_sync();
     }
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < G.H * C; idx += kBlock) {
-      const int p = idx / C, c = idx - p * C, k = k0 + c;
-      if (k < G.Qh) spec[(size_t)p * G.Qh + k] = lds[c * stride + p];
-    }
-    __syncthreads();
   }
+  __syncthreads();
 }
 
 // --------------------------------------------------------------- projection

@@ -204,6 +204,99 @@ BSGP_HD cd c2r_gather(const cd* A, const cd* B, int Q, int Qh, int k) {
   return cmk(a.x + b.y, b.x - a.y);
 }
 
+// ---- compile-time transforms for the hot lengths ----------------------------
+// Same Stockham stages, but with n, every radix and every span Ns known at
+// compile time: the butterfly loops unroll, j % Ns and j / Ns become shifts or
+// constant multiplies, and the stage sequence is straight-line code.
+struct RadixList {
+  int n;
+  int r[kMaxStages];
+};
+
+constexpr RadixList factor_radices(int n) {
+  RadixList L{0, {}};
+  int m = n;
+  while (m % 4 == 0) { L.r[L.n++] = 4; m /= 4; }
+  while (m % 2 == 0) { L.r[L.n++] = 2; m /= 2; }
+  while (m % 3 == 0) { L.r[L.n++] = 3; m /= 3; }
+  while (m % 5 == 0) { L.r[L.n++] = 5; m /= 5; }
+  return L;
+}
+
+template <int R, int N, int Ns>
+BSGP_HD void stage_static(const cd* in, cd* out, const cd* tw, bool inv, int lane, int nlanes) {
+  constexpr int nb = N / R;
+  constexpr int twstep = N / (Ns * R);
+#pragma unroll 1
+  for (int j0 = 0; j0 < nb; j0 += 64) {
+    const int j = j0 + lane;
+    if (nlanes == 64 ? (j < nb) : false) {
+      const int jm = j % Ns;
+      cd v[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = in[j + r * nb];
+      if constexpr (Ns > 1) {
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw_at(tw, r * jm * twstep, inv));
+      }
+      if constexpr (R == 2) bfly2(v);
+      if constexpr (R == 3) bfly3(v, inv);
+      if constexpr (R == 4) bfly4(v, inv);
+      if constexpr (R == 5) bfly5(v, inv);
+      const int od = (j / Ns) * Ns * R + jm;
+#pragma unroll
+      for (int r = 0; r < R; ++r) out[od + r * Ns] = v[r];
+    }
+  }
+  if (nlanes != 64) {  // host test path: serial lanes
+    for (int j = lane; j < nb; j += nlanes) {
+      const int jm = j % Ns;
+      cd v[R];
+      for (int r = 0; r < R; ++r) v[r] = in[j + r * nb];
+      if (Ns > 1)
+        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw_at(tw, r * jm * twstep, inv));
+      if constexpr (R == 2) bfly2(v);
+      if constexpr (R == 3) bfly3(v, inv);
+      if constexpr (R == 4) bfly4(v, inv);
+      if constexpr (R == 5) bfly5(v, inv);
+      const int od = (j / Ns) * Ns * R + jm;
+      for (int r = 0; r < R; ++r) out[od + r * Ns] = v[r];
+    }
+  }
+}
+
+template <int N, int S, int Ns, class Sync>
+BSGP_HD cd* stages_static(cd* in, cd* out, const cd* tw, bool inv, int lane, int nlanes,
+                          Sync sync) {
+  constexpr RadixList L = factor_radices(N);
+  if constexpr (S < L.n) {
+    constexpr int R = L.r[S];
+    stage_static<R, N, Ns>(in, out, tw, inv, lane, nlanes);
+    sync();
+    return stages_static<N, S + 1, Ns * R>(out, in, tw, inv, lane, nlanes, sync);
+  } else {
+    return in;
+  }
+}
+
+// Transform of compile-time length N (must be 2/3/5-smooth).
+template <int N, class Sync>
+BSGP_HD cd* fft_run_static(cd* a, cd* b, const cd* tw, bool inv, int lane, int nlanes, Sync sync) {
+  static_assert(factor_radices(N).n > 0, "N must be 2/3/5-smooth");
+  return stages_static<N, 0, 1>(a, b, tw, inv, lane, nlanes, sync);
+}
+
+// Runtime length with compile-time fast paths for the hot grid sizes
+// (256: circular 256^2; 270: 256^2 image with a 25x25 PSF, linear mode).
+template <class Sync>
+BSGP_HD cd* fft_any(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlanes, Sync sync) {
+  switch (p.n) {
+    case 256: return fft_run_static<256>(a, b, p.tw, inv, lane, nlanes, sync);
+    case 270: return fft_run_static<270>(a, b, p.tw, inv, lane, nlanes, sync);
+    default: return fft_run(a, b, p, inv, lane, nlanes, sync);
+  }
+}
+
 // Factor n into stage radices: 4s first, then 2, 3, 5, then remaining primes.
 // Returns false when n needs more than kMaxStages stages or n < 1.
 inline bool plan_radices(int n, int* radix, int* ns) {

@@ -11,7 +11,8 @@ namespace bsgp {
 
 // Per-image solver state carried between the phase kernels (device memory).
 struct ImgState {
-  int par, Xones, stop, iter, epoch, pad_;
+  int par, Xones, stop, iter, epoch;
+  int bar_base;  // team-barrier counter value at the start of the next kernel (T > 1)
   int64_t E_p, E_ls, ls_passes, status, ls_series;
   double sc, flux, bks_scalar, lo, hi, Dcoeff, tol, t0;
   double fv, alpha, tau, lr, init_lr, beta, lam_p, gd, lam;
@@ -35,6 +36,11 @@ struct SolveArgs {
   size_t slot_stride;  // doubles per slot
   size_t vec_stride;   // doubles per image vector (N rounded up to 32)
   size_t lds_fft_bytes;
+  // teams (T workgroups per image; T = 1: one workgroup, none of these used)
+  int T;
+  double* tpart;        // [B][2][T][kMaxRed] reduction partials
+  unsigned int* tctr;   // [B] barrier arrival counters, zeroed per solve
+  int* tfail;           // set by a timed-out barrier spin
 };
 
 hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s);

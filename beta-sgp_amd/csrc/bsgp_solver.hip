@@ -31,18 +31,18 @@ __device__ __forceinline__ double realtime_s() {
 // U pairs before computing any of them (memory-level parallelism for one
 // workgroup streaming a whole image).  `ld(p)` loads, `cp(p, v)` computes.
 template <int U, class LD, class CP>
-__device__ __forceinline__ void stream2(int npair, LD&& ld, CP&& cp) {
+__device__ __forceinline__ void stream2(const Part& D, int npair, LD&& ld, CP&& cp) {
   using T = decltype(ld(0));
-  for (int b = threadIdx.x; b < npair; b += kBlock * U) {
+  for (int b = D.gt0 + threadIdx.x; b < npair; b += D.gts * U) {
     T v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int p = b + u * kBlock;
+      const int p = b + u * D.gts;
       if (p < npair) v[u] = ld(p);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int p = b + u * kBlock;
+      const int p = b + u * D.gts;
       if (p < npair) cp(p, v[u]);
     }
   }
@@ -129,6 +129,30 @@ __device__ __forceinline__ Objective make_obj(const SolveArgs& A, double beta) {
   return o;
 }
 
+// Team of the workgroup: members blockIdx.x % T of image img0 + blockIdx.x / T.
+__device__ __forceinline__ Team make_team(const SolveArgs& A, int img, const ImgState& st) {
+  Team t;
+  t.T = A.T;
+  t.m = A.T == 1 ? 0 : (int)(blockIdx.x % (unsigned)A.T);
+  t.part = A.tpart ? A.tpart + (size_t)img * 2 * A.T * kMaxRed : nullptr;
+  t.ctr = A.tctr ? A.tctr + img : nullptr;
+  t.base = (unsigned int)st.bar_base;
+  t.nb = 0;
+  t.fail = A.tfail;
+  return t;
+}
+__device__ __forceinline__ int team_img(const SolveArgs& A) {
+  return A.img0 + (A.T == 1 ? (int)blockIdx.x : (int)(blockIdx.x / (unsigned)A.T));
+}
+// Member 0 records where the barrier counter stands for the next kernel; all
+// members read bar_base before their first arrival, member 0 writes it after
+// its last one, so no member can see the new value early.
+__device__ __forceinline__ void team_end(ImgState& st, const Team& t) {
+  if (t.T > 1 && t.m == 0 && threadIdx.x == 0 && t.nb > 0)
+    st.bar_base = (int)(t.base + (unsigned int)t.T * (unsigned int)t.nb);
+}
+__device__ __forceinline__ bool leader(const Team& t) { return t.m == 0 && threadIdx.x == 0; }
+
 #define BSGP_LDS_VIEWS(A)                                                           \
   extern __shared__ __attribute__((aligned(16))) char smem[];                      \
   cd* lds = reinterpret_cast<cd*>(smem);                                           \
@@ -139,7 +163,7 @@ __device__ __forceinline__ Objective make_obj(const SolveArgs& A, double beta) {
 // projection, x_tf = A(x), f, g and the scaling-matrix bounds.
 __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   BSGP_LDS_VIEWS(A);
-  const int img = A.img0 + blockIdx.x;
+  const int img = team_img(A);
   const Geo& G = A.g;
   const bsgp_params& P = A.prm;
   const int N = G.H * G.W;
@@ -148,6 +172,10 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   const bool odd = (N & 1) != 0;
   Bufs B = slot_bufs(A, img, 0);
   ImgState& st = A.st[img];
+  // counters are zeroed per solve: the setup kernel starts the count at 0
+  Team tm = make_team(A, img, st);
+  tm.base = 0;
+  const Part D = make_part(tm, G.nfw);
   const double* gn_in = A.in.gn + (size_t)img * N;
   const double* bk_in = bmap ? A.in.bkg + (size_t)img * N : nullptr;
   const double bk_scalar_raw = bmap ? 0.0 : A.in.bkg[img];
@@ -156,15 +184,15 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   // raw statistics (sgp.py:174-177, 190, 193-194)
   double v2[2] = {0.0, 0.0};  // sum(gn - bkg), sum(gn)
   double mx = -INFINITY;
-  for (int i = tid; i < N; i += kBlock) {
+  for (int i = D.gt0 + tid; i < N; i += D.gts) {
     const double g = gn_in[i];
     const double bkr = bmap ? bk_in[i] : bk_scalar_raw;
     v2[0] += g - bkr;
     v2[1] += g;
     mx = (g > mx || g != g) ? g : mx;
   }
-  block_sum<2>(v2, red);
-  mx = block_max(mx, red);
+  team_sum<2>(v2, red, tm);
+  mx = team_max(mx, red, tm);
   const double sc = P.scale_data == 2 ? P.prescaled_scaling : (P.scale_data ? mx : 1.0);
   const double fl_raw = A.in.flux ? A.in.flux[img] : v2[0];
   const double x3 = (fl_raw / (double)N) * 1.0;  // np.sum(gn-bkg)/gn.size*ones (sgp.py:175)
@@ -173,17 +201,17 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   const double bks_scalar = P.scale_data == 2 ? bk_scalar_raw : bk_scalar_raw / sc;
   // scale + null-pixel minimum (sgp.py:193-204)
   double vmin = INFINITY;
-  for (int i = tid; i < N; i += kBlock) {
+  for (int i = D.gt0 + tid; i < N; i += D.gts) {
     const double g = divide ? gn_in[i] / sc : gn_in[i];
     B.gns[i] = g;
     if (g > 0 && g < vmin) vmin = g;
     if (bmap) B.bks[i] = divide ? bk_in[i] / sc : bk_in[i];
   }
-  vmin = block_min(vmin, red);
+  vmin = team_min(vmin, red, tm);
   const double eps = 2.220446049250313e-16;
   const double fill = vmin * eps * eps;
   double v1[1] = {0.0};
-  for (int i = tid; i < N; i += kBlock) {
+  for (int i = D.gt0 + tid; i < N; i += D.gts) {
     double g = B.gns[i];
     if (g <= 0) {
       g = fill;
@@ -205,32 +233,38 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     if (P.proj_type == 0 && x < 0) x = 0;
     B.xa[i] = x;
   }
-  if (odd && tid == 0) {  // benign pad element of the pair-vectorised streams
+  if (odd && leader(tm)) {  // benign pad element of the pair-vectorised streams
     B.gns[N] = 1.0;
     if (bmap) B.bks[N] = 0.0;
     B.xa[N] = B.xb[N] = B.ga[N] = B.gb[N] = B.xtf[N] = B.dtf[N] = 0.0;
   }
-  block_sum<1>(v1, red);
+  team_sum<1>(v1, red, tm);
   const double flux = A.in.flux ? A.in.flux[img] / sc : v1[0];  // sgp.py:208-211
   const ProjClip clip{P.has_sat != 0, P.ccd_sat_level / sc - eps};
 
-  // initial projection with dia = 1 (sgp.py:250-253)
+  // initial projection with dia = 1 (sgp.py:250-253); every thread clips the
+  // pixels it wrote, so only the rows pass below needs the team barrier
   if (P.proj_type == 1) {
-    ProjOut po = project_df(
-        N, [&](int i, double& c, double& dia) { c = B.xa[i]; dia = 1.0; }, clip, flux, 0.0, 1.0,
-        1e-11, 0, 0, P.max_projs, red);
-    for (int i = tid; i < N; i += kBlock) B.xa[i] = clip(B.xa[i], 1.0, po.lam);
-    __syncthreads();
+    auto psum = [&](double lam) {
+      double s1[1] = {0.0};
+      for (int i = D.gt0 + tid; i < N; i += D.gts) s1[0] += clip(B.xa[i], 1.0, lam);
+      team_sum<1>(s1, red, tm);
+      return s1[0];
+    };
+    ProjOut po = project_df_fn(psum, flux, 0.0, 1.0, 1e-11, 0, 0, P.max_projs);
+    for (int i = D.gt0 + tid; i < N; i += D.gts) B.xa[i] = clip(B.xa[i], 1.0, po.lam);
   }
+  team_barrier(tm);  // x0 / gns / bks complete before the row passes
   // x_tf = A(x), f and g (sgp.py:260-265 / 702-709)
   const double beta0 = A.in.beta0 ? A.in.beta0[img] : P.betaParam;
   Objective obj = make_obj(A, beta0);
   double fsum[3] = {0.0, 0.0, 0.0};  // K, T0, T1
-  row_fwd(G, G.H, G.W, B.spec, lds, [&](int r, int j) { return B.xa[r * G.W + j]; });
-  __syncthreads();
-  col_conv(G, B.spec, G.tfA, lds);
+  row_fwd(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.xa[r * G.W + j]; });
+  team_barrier(tm);
+  col_conv(G, D, B.spec, G.tfA, lds);
+  team_barrier(tm);
   const bool beta_obj = P.variant == BSGP_VARIANT_BETA;
-  row_inv_fwd(G, B.spec, lds, [&](int r, int j, double v) {
+  row_inv_fwd(G, D, B.spec, lds, [&](int r, int j, double v) {
     const int i = r * G.W + j;
     B.xtf[i] = v;
     const double den = v + (bmap ? B.bks[i] : bks_scalar);
@@ -242,28 +276,30 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     B.pw[i] = p;
     return g * (p / den);  // gn*den^(b-2) (sgp.py:499)
   });
-  block_sum<3>(fsum, red);  // its barrier publishes xtf / spec
+  team_sum<3>(fsum, red, tm);  // its barrier publishes xtf / spec
   const double fv = obj.combine(fsum[0], fsum[1], fsum[2], flux, (double)N);
-  col_conv(G, B.spec, G.tfAT, lds);
-  row_inv(G, B.spec, lds, [&](int r, int j, double at) {
+  col_conv(G, D, B.spec, G.tfAT, lds);
+  team_barrier(tm);
+  row_inv(G, D, B.spec, lds, [&](int r, int j, double at) {
     const int i = r * G.W + j;
     B.ga[i] = (beta_obj ? B.pw[i] : 1.0) - at;  // sgp.py:263 / 499
   });
-  __syncthreads();
+  team_barrier(tm);  // every row of spec read before it is overwritten
   // scaling-matrix bounds from AT(gn) (sgp.py:268-273)
-  row_fwd(G, G.H, G.W, B.spec, lds, [&](int r, int j) { return B.gns[r * G.W + j]; });
-  __syncthreads();
-  col_conv(G, B.spec, G.tfAT, lds);
+  row_fwd(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.gns[r * G.W + j]; });
+  team_barrier(tm);
+  col_conv(G, D, B.spec, G.tfAT, lds);
+  team_barrier(tm);
   double ymin = INFINITY, ymax = -INFINITY;
-  row_inv(G, B.spec, lds, [&](int r, int j, double at) {
+  row_inv(G, D, B.spec, lds, [&](int r, int j, double at) {
     const int i = r * G.W + j;
     const double bkv = bmap ? B.bks[i] : bks_scalar;
     const double y = (flux / (flux + bkv)) * at;
     if (y > 0 && y < ymin) ymin = y;
     ymax = (y > ymax || y != y) ? y : ymax;
   });
-  ymin = block_min(ymin, red);
-  ymax = block_max(ymax, red);
+  ymin = team_min(ymin, red, tm);
+  ymax = team_max(ymax, red, tm);
   double lo = ymin, hi = ymax;
   if (hi / lo < 50) {
     lo = lo / 10;
@@ -273,7 +309,7 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   double tol = P.tol_convergence;
   if (P.stop_criterion == 4) tol = tol4;
   if (P.verbose && P.stop_criterion == 2) tol = tol * tol;
-  if (tid == 0) {
+  if (leader(tm)) {
     const int M1 = P.MAXIT + 1;
     A.out.discr[(size_t)img * M1] = Dcoeff * fv;
     if (A.out.times) A.out.times[(size_t)img * M1] = 0.0;
@@ -286,6 +322,7 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     st.stop = 0;
     st.iter = 1;
     st.epoch = 0;
+    st.bar_base = (int)((unsigned int)tm.T * (unsigned int)tm.nb);
     st.E_p = st.E_ls = st.ls_passes = st.status = st.ls_series = 0;
     st.sc = sc;
     st.flux = flux;
@@ -312,17 +349,19 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
 // d.g, and the row transforms of d.
 __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
   BSGP_LDS_VIEWS(A);
-  const int img = A.img0 + blockIdx.x;
+  const int img = team_img(A);
   ImgState& st = A.st[img];
   if (st.stop) return;
+  Team tm = make_team(A, img, st);
   const Geo& G = A.g;
+  const Part Pt = make_part(tm, G.nfw);
   const bsgp_params& P = A.prm;
   const int N = G.H * G.W;
   const int npair = (N + 1) / 2;
   const bool odd = (N & 1) != 0;
-  const int tid = threadIdx.x;
   Bufs B = slot_bufs(A, img, st.par);
   Dir D = make_dir(A, st);
+  const double flux = st.flux;
   int evals = 0;
   if (P.proj_type == 1) {
     const double* xa = B.xa;
@@ -330,7 +369,7 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
     auto psum = [&](double lam) {
       double s[1] = {0.0};
       stream2<4>(
-          npair,
+          Pt, npair,
           [&](int p) {
             struct V {
               double2 x, g;
@@ -348,23 +387,24 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
               s[0] += D.clip(c, d, lam);
             }
           });
-      block_sum<1>(s, red);
+      team_sum<1>(s, red, tm);
       return s[0];
     };
-    ProjOut po = project_df_fn(psum, st.flux, 0.0, 1.0, 1e-11, 0, 0, P.max_projs);
+    ProjOut po = project_df_fn(psum, flux, 0.0, 1.0, 1e-11, 0, 0, P.max_projs);
     D.lam_p = po.lam;
     evals = po.evals;
   }
   double gd[1] = {0.0};
-  row_fwd(G, G.H, G.W, B.spec, lds, [&](int r, int j) {
+  row_fwd(G, Pt, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) {
     const int i = r * G.W + j;
     const double g = B.ga[i];
     const double d = D.d(B.xa[i], g);
     gd[0] += d * g;
     return d;
   });
-  block_sum<1>(gd, red);
-  if (tid == 0) {  // sgp.py:306-308 (memory shifts) + direction scalars
+  team_sum<1>(gd, red, tm);
+  team_end(st, tm);
+  if (leader(tm)) {  // sgp.py:306-308 (memory shifts) + direction scalars
     for (int k = 0; k < P.M_alpha - 1; ++k) st.Valpha[k] = st.Valpha[k + 1];
     for (int k = 0; k < P.M - 1; ++k) st.Fold[k] = st.Fold[k + 1];
     st.Fold[P.M - 1] = st.fv;
@@ -378,10 +418,12 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
 // ----------------------------------------------------------- kernel: columns
 __global__ void __launch_bounds__(kBlock) k_col(SolveArgs A, int transpose) {
   BSGP_LDS_VIEWS(A);
-  const int img = A.img0 + blockIdx.x;
-  if (A.st[img].stop) return;
+  const int img = team_img(A);
+  const ImgState& st = A.st[img];
+  if (st.stop) return;
+  const Team tm = make_team(A, img, st);
   Bufs B = slot_bufs(A, img, 0);
-  col_conv(A.g, B.spec, transpose ? A.g.tfAT : A.g.tfA, lds);
+  col_conv(A.g, make_part(tm, A.g.nfw), B.spec, transpose ? A.g.tfAT : A.g.tfA, lds);
 }
 
 // ------------------------------- kernel: line search + accept + rows of w
@@ -394,16 +436,18 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
   // which is where most non-stagnating iterations accept; later passes
   // stream K trial lambdas each.
   BSGP_LDS_VIEWS(A);
-  const int img = A.img0 + blockIdx.x;
+  const int img = team_img(A);
   ImgState& st = A.st[img];
   if (st.stop) return;
+  Team tm = make_team(A, img, st);
   const Geo& G = A.g;
+  const Part Pt = make_part(tm, G.nfw);
   const bsgp_params& P = A.prm;
   const int N = G.H * G.W;
   const int npair = (N + 1) / 2;
   const bool odd = (N & 1) != 0;
-  const int tid = threadIdx.x;
   const bool bmap = P.bkg_is_map != 0;
+  const double lr_st = st.lr;
   constexpr bool adapt = ADAPT;  // adaptive beta (sgp.py:798-800): K == 1, runtime mode
   Bufs B = slot_bufs(A, img, st.par);
   const double bks_scalar = st.bks_scalar;
@@ -438,7 +482,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
 #pragma unroll
     for (int k = 0; k < N1; ++k) t1[k] = 0.0;
     double umax = 0.0;
-    row_inv(G, B.spec, lds, [&](int r, int j, double v) {
+    row_inv(G, Pt, B.spec, lds, [&](int r, int j, double v) {
       const int i = r * G.W + j;
       B.dtf[i] = v;
       const double g = B.gns[i];
@@ -466,8 +510,8 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
         umax = (au > umax || au != au || !(a > 0)) ? (a > 0 ? au : INFINITY) : umax;
       }
     });
-    block_sum<N1>(t1, red);
-    if (series) rho = block_max(umax, red);
+    team_sum<N1>(t1, red, tm);
+    if (series) rho = team_max(umax, red, tm);
 #pragma unroll
     for (int m = 0; m <= MS; ++m) {
       Pm[m] = t1[4 + m];
@@ -484,7 +528,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
       lam = lam * P.beta;
       if (adapt) {  // sgp.py:798-800: beta -= lr * mean(dDiv/dbeta)
         const double bgrad = (obj.beta == 0.0 || obj.beta == 1.0) ? 0.0 : t1[3] / N;
-        obj.set_beta(obj.beta - st.lr * bgrad);
+        obj.set_beta(obj.beta - lr_st * bgrad);
       }
     }
   }
@@ -548,7 +592,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
     const double* gns = B.gns;
     const double* bks = B.bks;
     stream2<1>(
-        npair,
+        Pt, npair,
         [&](int p) {
           struct V {
             double2 x, d, g, b;
@@ -563,7 +607,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
           eval_px(v.x.x, v.d.x, v.g.x, v.b.x);
           if (!odd || 2 * p + 1 < N) eval_px(v.x.y, v.d.y, v.g.y, v.b.y);
         });
-    block_sum<NT>(t, red);
+    team_sum<NT>(t, red, tm);
     if (adapt) konst = t[2 * K];
     ++passes;
 #pragma unroll
@@ -582,7 +626,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
     lam = lamk[K - 1] * P.beta;
     if (adapt) {  // sgp.py:798-800: beta -= lr * mean(dDiv/dbeta)   (K == 1 here)
       const double bgrad = (obj.beta == 0.0 || obj.beta == 1.0) ? 0.0 : t[2 * K + 1] / N;
-      obj.set_beta(obj.beta - st.lr * bgrad);
+      obj.set_beta(obj.beta - lr_st * bgrad);
     }
     if (nls > 64) {  // unreachable: lam < 1e-12 forces acceptance by the 32nd trial
       status = 1;
@@ -591,7 +635,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
   }
   // accept: x_tf += lam*d_tf; w = gn/den or gn*den^(b-2) (sgp.py:337-345, 790)
   const double lam_acc = lam;
-  row_fwd(G, G.H, G.W, B.spec, lds, [&](int r, int j) {
+  row_fwd(G, Pt, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) {
     const int i = r * G.W + j;
     const double xt = B.xtf[i] + lam_acc * B.dtf[i];
     B.xtf[i] = xt;
@@ -602,7 +646,8 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
     B.pw[i] = p;
     return g * (p / den);
   });
-  if (tid == 0) {
+  team_end(st, tm);
+  if (leader(tm)) {
     if (A.out.flags)
       A.out.flags[(size_t)img * (P.MAXIT + 1) + st.iter] = (f_acc >= fr) ? 1 : 0;
     st.fv = f_acc;
@@ -622,23 +667,32 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
 // and the outputs once the image stops (sgp.py:424-438).
 __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
   BSGP_LDS_VIEWS(A);
-  const int img = A.img0 + blockIdx.x;
+  const int img = team_img(A);
   ImgState& st = A.st[img];
   if (st.stop) return;
+  Team tm = make_team(A, img, st);
   const Geo& G = A.g;
+  const Part Pt = make_part(tm, G.nfw);
   const bsgp_params& P = A.prm;
   const int N = G.H * G.W;
   const int tid = threadIdx.x;
-  const bool bmap = P.bkg_is_map != 0;
   const bool beta_obj = P.variant == BSGP_VARIANT_BETA;
   Bufs B = slot_bufs(A, img, st.par);
   Dir D = make_dir(A, st);
   const double lam = st.lam;
-  const double bks_scalar = st.bks_scalar;
-  Objective obj = make_obj(A, st.beta);
   const double lo = st.lo, hi = st.hi;
+  // every state value the members use is read before the first team barrier:
+  // member 0 rewrites the state after the last one
+  const double alpha = st.alpha;
+  double vmin_ring = INFINITY;  // min(Valpha[0 .. M_alpha-2])
+  for (int k = 0; k < P.M_alpha - 1; ++k) vmin_ring = k ? py_min2(vmin_ring, st.Valpha[k]) : st.Valpha[0];
+  const int iter = st.iter;
+  const double tau0 = st.tau, init_lr = st.init_lr, lr0 = st.lr;
+  const int epoch = st.epoch;
+  const double fv = st.fv, Dcoeff = st.Dcoeff, tol = st.tol, fold_last = st.Fold[P.M - 1];
+  const double sc = st.sc;
   double bb[6] = {0, 0, 0, 0, 0, 0};  // bk, ck, sk2.sk2, yk2.yk2, sk.sk, x.x
-  row_inv(G, B.spec, lds, [&](int r, int j, double at) {
+  row_inv(G, Pt, B.spec, lds, [&](int r, int j, double at) {
     const int i = r * G.W + j;
     const double gnew = (beta_obj ? B.pw[i] : 1.0) - at;  // sgp.py:342 / 790
     const double x = B.xa[i], g = B.ga[i];
@@ -659,9 +713,8 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
     B.xb[i] = xn;
     B.gb[i] = gnew;
   });
-  block_sum<6>(bb, red);
+  team_sum<6>(bb, red, tm);
   // Barzilai-Borwein (sgp.py:366-386)
-  const double alpha = st.alpha;
   double alpha1, alpha2;
   if (bb[0] <= 0) {
     alpha1 = py_min2(10 * alpha, P.alpha_max);
@@ -673,11 +726,8 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
   } else {
     alpha2 = py_min2(P.alpha_max, py_max2(P.alpha_min, bb[1] / bb[3]));
   }
-  double vmin = P.M_alpha > 1 ? st.Valpha[0] : alpha2;  // python min(Valpha)
-  for (int k = 1; k < P.M_alpha - 1; ++k) vmin = py_min2(vmin, st.Valpha[k]);
-  if (P.M_alpha > 1) vmin = py_min2(vmin, alpha2);
-  const int iter = st.iter;
-  double tau = st.tau, anew;
+  const double vmin = P.M_alpha > 1 ? py_min2(vmin_ring, alpha2) : alpha2;  // python min(Valpha)
+  double tau = tau0, anew;
   if (iter <= 20) {
     anew = vmin;
   } else if (alpha2 / alpha1 < tau) {
@@ -688,20 +738,18 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
     tau = tau * 1.1;
   }
   const double lr = (P.variant == BSGP_VARIANT_BETA && P.schedule_lr)
-                        ? st.init_lr * exp(-P.lr_exp_param * st.epoch)
-                        : st.lr;
+                        ? init_lr * exp(-P.lr_exp_param * epoch)
+                        : lr0;
   // stop rules (sgp.py:390-414)
   const int it2 = iter + 1;
   bool loop = true;
   double crit = 0.0;
-  const double fv = st.fv;
-  const double dk = st.Dcoeff * fv;
-  const double tol = st.tol;
+  const double dk = Dcoeff * fv;
   if (P.stop_criterion == 2) {
     crit = bb[4] / bb[5];
     loop = crit > tol;
   } else if (P.stop_criterion == 3) {
-    crit = (st.Fold[P.M - 1] - fv) / fv;
+    crit = (fold_last - fv) / fv;
     loop = crit > tol && crit >= 0;
   } else if (P.stop_criterion == 4) {
     crit = dk;
@@ -710,12 +758,11 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
   if (it2 > P.MAXIT) loop = false;
   if (!loop) {
     // outputs: x reverts to prev_x = xa (sgp.py:424-438, 892-895)
-    const double sc = st.sc;
     double* xo = A.out.x + (size_t)img * N;
-    for (int i = tid; i < N; i += kBlock) xo[i] = B.xa[i] * sc;
+    for (int i = Pt.gt0 + tid; i < N; i += Pt.gts) xo[i] = B.xa[i] * sc;
   }
-  __syncthreads();  // every thread has read st before thread 0 rewrites it
-  if (tid == 0) {
+  team_end(st, tm);
+  if (leader(tm)) {
     const size_t M1 = (size_t)P.MAXIT + 1;
     A.out.discr[img * M1 + it2 - 1] = dk;
     if (A.out.times) A.out.times[img * M1 + it2 - 1] = realtime_s() - st.t0;
@@ -737,9 +784,12 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
         c[0] = st.E_p;
         c[1] = st.E_ls;
         c[2] = st.ls_passes;
-        c[3] = st.status;
+        c[3] = st.status |
+               ((A.tfail && __hip_atomic_load(A.tfail, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT)) ? 4 : 0);
         c[4] = st.ls_series;
-        c[5] = c[6] = c[7] = 0;
+        c[5] = tm.T;
+        c[6] = c[7] = 0;
       }
       atomicSub(A.active, 1);
     }
@@ -753,26 +803,24 @@ __global__ void __launch_bounds__(kBlock) build_tf_kernel(Geo G, const double* k
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cd* lds = reinterpret_cast<cd*>(smem);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  row_fwd(G, G.P, G.Q, spec, lds, [&](int r, int j) { return kc[r * G.Q + j]; });
+  // rows of the P x Q kernel grid -> column-major half spectrum (ld = P)
+  row_fwd(G, solo_part(G.nfw), G.P, G.Q, G.P, spec, lds,
+          [&](int r, int j) { return kc[r * G.Q + j]; });
   __syncthreads();
-  const int C = G.nfw;
-  const int stride = 2 * G.lpad;
-  for (int k0 = 0; k0 < G.Qh; k0 += C) {
-    for (int idx = threadIdx.x; idx < G.P * C; idx += kBlock) {
-      const int p = idx / C, c = idx - p * C, k = k0 + c;
-      lds[c * stride + p] = (k < G.Qh) ? spec[(size_t)p * G.Qh + k] : cmk(0.0, 0.0);
-    }
-    __syncthreads();
-    if (w < C && k0 + w < G.Qh) {
-      cd* a = lds + w * stride;
-      cd* Z = fft_run(a, a + G.lpad, G.fp, false, lane, 64, WaveSync());
-      cd* t = tf + (size_t)(k0 + w) * G.P;
+  if (w < G.nfw) {
+    cd* a = lds + w * 2 * G.lpad;
+    for (int k = w; k < G.Qh; k += G.nfw) {
+      const cd* col = spec + (size_t)k * G.P;
+      for (int p = lane; p < G.P; p += 64) a[p] = col[p];
+      wave_sync();
+      cd* Z = fft_any(a, a + G.lpad, G.fp, false, lane, 64, WaveSync());
+      cd* t = tf + (size_t)k * G.P;
       for (int p = lane; p < G.P; p += 64) {
         cd z = cscale(Z[p], scale);
         t[p] = conj ? cconj(z) : z;
       }
+      wave_sync();
     }
-    __syncthreads();
   }
 }
 
@@ -787,10 +835,11 @@ __global__ void __launch_bounds__(kBlock) apply_op_kernel(Geo G, int B, int tran
   for (int img = blockIdx.x; img < B; img += gridDim.x) {
     const double* xi = x + (size_t)img * N;
     double* oi = out + (size_t)img * N;
-    row_fwd(G, G.H, G.W, spec, lds, [&](int r, int j) { return xi[r * G.W + j]; });
+    const Part D = solo_part(G.nfw);
+    row_fwd(G, D, G.H, G.W, G.H, spec, lds, [&](int r, int j) { return xi[r * G.W + j]; });
     __syncthreads();
-    col_conv(G, spec, transpose ? G.tfAT : G.tfA, lds);
-    row_inv(G, spec, lds, [&](int r, int j, double v) { oi[r * G.W + j] = v; });
+    col_conv(G, D, spec, transpose ? G.tfAT : G.tfA, lds);
+    row_inv(G, D, spec, lds, [&](int r, int j, double v) { oi[r * G.W + j] = v; });
     __syncthreads();
   }
 }
@@ -850,11 +899,11 @@ __global__ void grad_parts_kernel(int64_t n, const double* den, const double* gn
 
 // ----------------------------------------------------------- launchers
 hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL(k_setup, dim3(a.nimg), dim3(kBlock), lds, s, a);
+  hipLaunchKernelGGL(k_setup, dim3(a.nimg * a.T), dim3(kBlock), lds, s, a);
   return hipGetLastError();
 }
 hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
-  const dim3 grid(a.nimg), block(kBlock);
+  const dim3 grid(a.nimg * a.T), block(kBlock);
   hipLaunchKernelGGL(k_dir, grid, block, lds, s, a);
   hipLaunchKernelGGL(k_col, grid, block, lds, s, a, 0);
   // line-search kernel specialised on trial width, objective mode, adaptivity

@@ -46,6 +46,7 @@ DEFAULT_COLUMNS = ['label', 'xcentroid', 'ycentroid', 'sky_centroid',
 LS_SPEC_DEFAULT = 2  # line-search trial lambdas evaluated per pass over the data
 LS_SERIES_DEFAULT = 1  # small line-search steps from the moment series (general beta)
 STREAMS_DEFAULT = 2  # sub-batch streams of a batched solve
+TEAM_DEFAULT = 0  # workgroups per image: 0 = auto (spread small batches over the CUs)
 
 
 # ------------------------------------------------------------------ helpers
@@ -98,7 +99,8 @@ def _prelude_host(gn, bkg, init_recon, flux, stop_criterion, scale_data):
 def _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, alpha, alpha_min,
             alpha_max, M_alpha, tau, M, max_projs, verbose, ccd_sat_level, scale_data,
             tol_convergence, adapt_beta=False, betaParam=1.005, lr=1e-3, lr_exp_param=0.1,
-            schedule_lr=False, bkg_is_map=False, ls_spec=None, ls_series=None, streams=None):
+            schedule_lr=False, bkg_is_map=False, ls_spec=None, ls_series=None, streams=None,
+            team=None):
     p = _B.Params()
     p.variant = variant
     p.init_recon = int(init_recon)
@@ -123,6 +125,7 @@ def _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, 
     p.ls_spec = 1 if (variant == _B.BSGP_VARIANT_BETA and adapt_beta) else ls
     p.ls_series = LS_SERIES_DEFAULT if ls_series is None else int(bool(ls_series))
     p.streams = STREAMS_DEFAULT if streams is None else int(streams)
+    p.team = TEAM_DEFAULT if team is None else int(team)
     return p
 
 
@@ -203,6 +206,7 @@ def _run(variant, gn, psf, bkg, init_recon, proj_type, stop_criterion, MAXIT, ga
     xd = None if x0 is None else _B.to_dev(np.asarray(x0, dtype=np.float64).reshape(1, *_shape))
     out = plan.solve(gd, bd, prm, flux=fd, x0=xd)
     _B.torch.cuda.current_stream().synchronize()
+    _B.check_status(out["counters"])
     it = int(out["iters"][0])
     discr = out["discr"][0, :it + 1].cpu().numpy()
     times = out["times"][0, :it + 1].cpu().numpy()
@@ -294,7 +298,7 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
                  ccd_sat_level=None, scale_data=True, tol_convergence=1e-4,
                  use_original_SGP_Afunction=True, adapt_beta=False, betaParam=1.005, lr=1e-3,
                  lr_exp_param=0.1, schedule_lr=False, ls_spec=None, ls_series=None,
-                 streams=None, device_out=False):
+                 streams=None, team=None, device_out=False):
     _check_psf(np.asarray(psf))
     torch = _B.torch
     _B.require_gpu()
@@ -311,7 +315,8 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
                   alpha_min, alpha_max, M_alpha, tau, M, max_projs, verbose, ccd_sat_level,
                   scale_data, tol_convergence, adapt_beta=adapt_beta, betaParam=betaParam, lr=lr,
                   lr_exp_param=lr_exp_param, schedule_lr=schedule_lr, bkg_is_map=bkg_is_map,
-                  ls_spec=ls_spec, ls_series=ls_series, streams=streams)
+                  ls_spec=ls_spec, ls_series=ls_series, streams=streams,
+                  team=team)
     x0 = None
     if init_recon == 1:
         np.random.seed(42)
@@ -325,6 +330,7 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
     if device_out:
         return out
     torch.cuda.current_stream().synchronize()
+    _B.check_status(out["counters"])
     return {k: (v.cpu().numpy() if v is not None else None) for k, v in out.items()}
 
 

@@ -77,7 +77,9 @@ typedef struct {
   int32_t ls_spec;        /* line-search lambdas evaluated per pass (1..8); 1 when adapt_beta */
   int32_t ls_series;      /* 1: small trial steps from the moment series (general beta) */
   int32_t streams;        /* sub-batches run on this many streams (1..4) so phases overlap */
-  int32_t reserved;
+  int32_t team;           /* workgroups cooperating on one image: 0 = auto (spread the
+                             batch over the CUs when B is small), 1 = one per image,
+                             k > 1 = at most k (capped so every workgroup is resident) */
 } bsgp_params;
 
 /* Device inputs of a batched solve. */
@@ -99,8 +101,10 @@ typedef struct {
   int32_t* flags;      /* [B][MAXIT1] bit0: fv >= fr warning (sgp.py:351), may be NULL */
   double* beta_final;  /* [B] final betaParam (sgp.py:892), may be NULL           */
   int64_t* counters;   /* [B][8]: proj evals E_p, line-search trials E_ls,
-                          line-search passes over the image, status bits, trials
-                          evaluated from the small-step series, 3 reserved; may be NULL */
+                          line-search passes over the image, status bits (1: line
+                          search cap, 4: team barrier timed out), trials evaluated
+                          from the small-step series, team size T, 2 reserved;
+                          may be NULL */
 } bsgp_outputs;
 
 /* Plan: geometry, FFT sizes, twiddles and the PSF transfer functions for A and

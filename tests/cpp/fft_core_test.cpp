@@ -83,6 +83,22 @@ int main() {
     for (int j = 0; j < Q; ++j) e2 = fmax(e2, fabs(zr[j].x / Q - ra[j]) + fabs(zr[j].y / Q - rb[j]));
     if (!(e1 < 1e-12 && e2 < 1e-14)) { printf("FAIL split Q=%d e1=%g e2=%g\n", Q, e1, e2); bad++; }
   }
+  // compile-time paths agree with the runtime plan bit for bit
+  for (int n : {256, 270}) {
+    for (int inv = 0; inv < 2; ++inv) {
+      FftPlan p;
+      p.n = n;
+      plan_radices(n, p.radix, &p.ns);
+      std::vector<cd> tw = twiddles(n);
+      p.tw = tw.data();
+      std::vector<cd> a(n), b(n), c(n), d(n);
+      for (int i = 0; i < n; ++i) c[i] = a[i] = cmk(rand() / (double)RAND_MAX, rand() / (double)RAND_MAX);
+      cd* r1 = fft_run(a.data(), b.data(), p, inv, 0, 1, [] {});
+      cd* r2 = fft_any(c.data(), d.data(), p, inv, 0, 1, [] {});
+      for (int i = 0; i < n; ++i)
+        if (r1[i].x != r2[i].x || r1[i].y != r2[i].y) { printf("FAIL static n=%d inv=%d i=%d\n", n, inv, i); bad++; break; }
+    }
+  }
   printf(bad ? "FFT core: %d failures\n" : "FFT core: all ok\n", bad);
   return bad ? 1 : 0;
 }

@@ -161,23 +161,65 @@ def test_solve_matches_reference_linear(name, sgpmod):
 
 
 # --------------------------------------------------------- batch properties
-def test_batch_is_bitwise_equal_to_single_solves(sgpmod):
-    """One workgroup per image: a batch result never depends on its neighbours."""
+@pytest.mark.parametrize("team", [1, 2])
+def test_batch_is_bitwise_equal_to_single_solves(sgpmod, team):
+    """Fixed team size (workgroups per image): a batch result never depends on
+    its neighbours, bit for bit."""
     fx = golden("ref_lin64_beta.npz")
     gn = fx["gn"].astype(np.float64)
     rng = np.random.default_rng(5)
     gns = np.stack([gn, np.roll(gn, 7, 0), gn[::-1].copy(), rng.poisson(gn).astype(np.float64)])
     kw = dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=12, alpha=10.0,
               ccd_sat_level=65000.0, use_original_SGP_Afunction=False, schedule_lr=True,
-              adapt_beta=False)
+              adapt_beta=False, team=team)
     betas = [1.05, 0.97, 1.0, 1.02]
     out = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, betaParams=betas, **kw)
+    assert np.all(out["counters"][:, 5] == team)
     for i in range(4):
-        x, it, discr, _, _ = sgpmod.sgp_betaDiv(gns[i], fx["psf"], np.float64(100.0),
-                                                betaParam=betas[i], **kw)
-        assert it == out["iters"][i]
-        np.testing.assert_array_equal(x, out["x"][i])
-        np.testing.assert_array_equal(discr, out["discr"][i, :it + 1])
+        one = sgpmod.sgp_betaDiv_batch(gns[i:i + 1], fx["psf"], 100.0, betaParams=betas[i:i + 1],
+                                       **kw)
+        assert one["iters"][0] == out["iters"][i]
+        np.testing.assert_array_equal(one["x"][0], out["x"][i])
+        np.testing.assert_array_equal(one["discr"][0], out["discr"][i])
+
+
+@pytest.mark.parametrize("name,teams", [("lin64_beta", [2, 3, 8]), ("lin256_kl", [5, 32]),
+                                        ("lin256_beta", [7, 32])])
+def test_team_sizes_match_reference(sgpmod, name, teams):
+    """T workgroups cooperating on one image (team barriers, per-member
+    partials): same iterates as the reference within the solve tolerance for
+    every team size, and the team size actually used is reported."""
+    fx = golden(f"ref_{name}.npz")
+    kw = ref_kwargs(fx)
+    if not np.isnan(fx["flux"]):
+        kw["flux"] = np.float64(fx["flux"])
+    bkg = float(fx["bkg"])
+    gns = fx["gn"].astype(np.float64)[None]
+    fn = sgpmod.sgp_betaDiv_batch if str(fx["fn"]) == "sgp_betaDiv" else sgpmod.sgp_batch
+    for T in teams:
+        out = fn(gns, fx["psf"], bkg, team=T, **kw)
+        assert out["counters"][0, 5] == T
+        assert out["counters"][0, 3] & 4 == 0
+        it = int(out["iters"][0])
+        assert it == int(fx["iters"])
+        assert rel(out["x"][0], fx["x"]) < SOLVE_RTOL, (T, rel(out["x"][0], fx["x"]))
+        np.testing.assert_allclose(out["discr"][0, :it + 1], fx["discr"], rtol=1e-7)
+
+
+def test_auto_team_spreads_small_batches(sgpmod):
+    """team=0 (default): a single image uses many workgroups, a batch as large
+    as the CU count uses one each."""
+    import torch
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    fx = golden("ref_lin64_beta.npz")
+    gn = fx["gn"].astype(np.float64)
+    kw = dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=3, alpha=10.0,
+              ccd_sat_level=65000.0, use_original_SGP_Afunction=False)
+    one = sgpmod.sgp_betaDiv_batch(gn[None], fx["psf"], 100.0, betaParams=[1.05], **kw)
+    assert one["counters"][0, 5] > 1
+    many = sgpmod.sgp_betaDiv_batch(np.broadcast_to(gn, (ncu, *gn.shape)).copy(), fx["psf"], 100.0,
+                                    betaParams=1.05, **kw)
+    assert np.all(many["counters"][:, 5] == 1)
 
 
 def test_flux_conservation_and_positivity_full_batch(sgpmod):
