@@ -47,12 +47,38 @@ def gaussian_psf(k, fwhm=None):
     return p / p.sum()
 
 
-def synth_batch(B, n, k, nstars, seed0, bkg=100.0):
+def embed_psf(psf, n):
+    """k x k PSF placed around (n//2, n//2) of an n x n array: the circular A
+    (sgp.py:108-120) needs psf.shape == image shape."""
+    k = psf.shape[0]
+    full = np.zeros((n, n))
+    o = n // 2 - k // 2
+    full[o:o + k, o:o + k] = psf
+    return full / full.sum()
+
+
+# SURVEY §8d configurations that fit one GPU (C1 is the reference's own
+# NGC7027 CPU case; C5 is C3 sharded over 8 GPUs = `--config c3 --gpus 8`).
+CONFIGS = {
+    "c2": dict(n=256, k=25, nstars=200, batch=1, circular=False,
+               desc="single {n}x{n} synthetic image, 25x25 Gaussian PSF, linear A"),
+    "c3": dict(n=256, k=25, nstars=200, batch=1024, circular=False,
+               desc="{B} independent {n}x{n} stamps per GPU, 25x25 PSF, linear A"),
+    "c4": dict(n=2048, k=64, nstars=5000, batch=1, circular=True,
+               desc="single {n}x{n} synthetic field, 64x64 PSF embedded at the centre, "
+                    "circular A (pow-2 FFT)"),
+}
+
+
+def synth_batch(B, n, k, nstars, seed0, bkg=100.0, circular=False):
     """SURVEY §8d synthetic stamps, generated on the device: point sources
     (pareto fluxes) blurred by the engine's own A, plus Poisson noise."""
     import _bsgp
     psf = gaussian_psf(k)
-    plan = _bsgp.get_plan(n, n, psf, _bsgp.BSGP_CONV_LINEAR_FILL)
+    if circular:
+        psf = embed_psf(psf, n)
+    plan = _bsgp.get_plan(n, n, psf, _bsgp.BSGP_CONV_CIRCULAR if circular
+                          else _bsgp.BSGP_CONV_LINEAR_FILL)
     pos = np.empty((B, nstars), dtype=np.int64)
     flx = np.empty((B, nstars))
     for i in range(B):
@@ -69,29 +95,30 @@ def synth_batch(B, n, k, nstars, seed0, bkg=100.0):
     return gn.contiguous(), psf
 
 
-def solve_kwargs(maxit, ls_spec, streams=None, team=None):
+def solve_kwargs(maxit, ls_spec, streams=None, team=None, circular=False):
     max_projs, gamma, beta, alpha_min, alpha_max, alpha, M_alpha, tau, M = (
         1000, 1e-4, 0.4, 1e-5, 1e5, 1e1, 3, 0.5, 1)  # sgp.DEFAULT_PARAMS (sgp.py:34)
     return dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=maxit, gamma=gamma, beta=beta,
                 alpha=alpha, alpha_min=alpha_min, alpha_max=alpha_max, M_alpha=M_alpha, tau=tau,
                 M=M, max_projs=max_projs, ccd_sat_level=65000.0, scale_data=True,
-                use_original_SGP_Afunction=False, adapt_beta=False, betaParam=1.05, lr=1e-3,
+                use_original_SGP_Afunction=circular, adapt_beta=False, betaParam=1.05, lr=1e-3,
                 lr_exp_param=0.1, schedule_lr=True, ls_spec=ls_spec, streams=streams,
                 team=team)
 
 
-def cpu_baseline(n, k, nstars, images, maxit, workers):
+def cpu_baseline(n, k, nstars, images, maxit, workers, circular=False):
     """Oracle (numpy port of the reference, oracle/sgp_oracle.py) on `images`
     stamps x `maxit` iterations, one image per task on `workers` processes;
     wall time of the solve phase (pool already warm, inputs built in-task)."""
     import cpu_bench
-    kw = solve_kwargs(maxit, None)
+    kw = solve_kwargs(maxit, None, circular=circular)
     kw.pop("ls_spec")
+    kw.pop("team")
     kw.pop("streams")
     iters, wall, cpu_s = cpu_bench.run_pool(n, k, nstars, images, kw, workers)
     return {"value": iters / wall, "unit": "image-iterations/s", "cores": workers,
             "kind": "port",
-            "sample": f"{images} stamps {n}x{n} (C3 generator) x {maxit} beta-SGP iterations "
+            "sample": f"{images} images {n}x{n} (bench generator) x {maxit} beta-SGP iterations "
                       f"with oracle/sgp_oracle.py on a pool of {workers} processes: "
                       f"{iters} image-iterations in {wall:.1f}s wall "
                       f"({iters / cpu_s:.1f} image-it/s per core)"}
@@ -131,7 +158,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c3", choices=["c3", "c2"])
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--maxit", type=int, default=100)
     ap.add_argument("--ls-spec", type=int, default=None)
@@ -160,11 +187,12 @@ def main():
     import _bsgp
     import sgp
 
-    n, k, nstars = 256, 25, 200
-    B = args.batch if args.batch else (1024 if args.config == "c3" else 1)
-    gn, psf = synth_batch(B, n, k, nstars, seed0=shard_seed0(rank, B))
+    cfg = CONFIGS[args.config]
+    n, k, nstars, circ = cfg["n"], cfg["k"], cfg["nstars"], cfg["circular"]
+    B = args.batch if args.batch else cfg["batch"]
+    gn, psf = synth_batch(B, n, k, nstars, seed0=shard_seed0(rank, B), circular=circ)
     bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
-    kw = solve_kwargs(args.maxit, args.ls_spec, args.streams, args.team)
+    kw = solve_kwargs(args.maxit, args.ls_spec, args.streams, args.team, circular=circ)
     torch.cuda.synchronize()
 
     def step():
@@ -217,8 +245,8 @@ def main():
         "dtype": "f64",
         "data": "synthetic (SURVEY §8d generator: pareto point sources * 25x25 Gaussian PSF "
                 "+ Poisson, bkg 100), built on device",
-        "config": {"workload": f"{args.config.upper()}: {B} independent {n}x{n} stamps per GPU, "
-                               f"beta-SGP (beta=1.05), linear A (25x25 PSF), proj_type=1, "
+        "config": {"workload": f"{args.config.upper()}: " + cfg["desc"].format(n=n, B=B)
+                               + f", beta-SGP (beta=1.05), proj_type=1, "
                                f"MAXIT={args.maxit}, stop_criterion=1",
                    "images_per_gpu": B, "image": [n, n], "psf": [k, k], "maxit": args.maxit,
                    "parallelism": f"{world} independent shards (no collective)",
@@ -238,8 +266,9 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         workers = max(1, min(16, os.cpu_count() or 1))
-        result["cpu_baseline"] = cpu_baseline(n, k, nstars, args.cpu_images, args.cpu_maxit,
-                                              workers)
+        images = args.cpu_images if B > 1 else 1
+        result["cpu_baseline"] = cpu_baseline(n, k, nstars, images, args.cpu_maxit,
+                                              min(workers, images), circular=circ)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

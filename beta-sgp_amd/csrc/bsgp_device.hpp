@@ -25,7 +25,7 @@ namespace bsgp {
 constexpr int kBlock = BSGP_BLOCK;  // threads per workgroup (one image per workgroup)
 constexpr int kWaves = kBlock / 64;
 constexpr int kMaxRed = 32;  // doubles reduced at once
-constexpr int kSharedBytes = 1024;  // LDS after the wave partials: reduced totals + scalars
+constexpr int kSharedBytes = 512;  // LDS after the wave partials: reduced totals + scalars
 
 // Geometry of one conv plan (P x Q FFT grid, H x W image).
 struct Geo {
@@ -39,6 +39,20 @@ struct Geo {
   const cd* tfA;   // [Qh][P] transfer function of A, scaled by 1/(P*Q)
   const cd* tfAT;  // [Qh][P] transfer function of AT
 };
+
+// Copy the twiddle tables of the static-length transforms into their LDS slot
+// (plan.lds_tw); the caller's next workgroup barrier publishes them.
+__device__ __forceinline__ void copy_tw(const FftPlan& f) {
+  if (f.lds_tw < 0) return;
+  extern __shared__ __attribute__((aligned(16))) char bsgp_dyn_lds[];
+  cd* d = reinterpret_cast<cd*>(bsgp_dyn_lds + f.lds_tw);
+  for (int i = threadIdx.x; i < f.n; i += kBlock) d[i] = f.tw[i];
+}
+__device__ __forceinline__ void load_tw_lds(const Geo& G) {
+  copy_tw(G.fp);
+  if (G.fq.lds_tw != G.fp.lds_tw) copy_tw(G.fq);
+  __syncthreads();
+}
 
 // --------------------------------------------------------------- syncs
 // LDS hand-off between lanes of ONE wavefront: wait for this wave's LDS ops
@@ -134,31 +148,52 @@ __device__ __forceinline__ double block_min(double v, double* red) {
 
 // --------------------------------------------------------------- teams
 // A team = T workgroups cooperating on one image (T = 1: one workgroup, no
-// global traffic).  Work is strided over the team's waves / threads; every
-// reduction is a team reduction: block totals -> per-member partials in
+// global traffic).  Rows (and columns) are strided over the team's waves;
+// every reduction is a team reduction: block totals -> per-member partials in
 // global memory -> team barrier -> fixed-order sum of the T partials, so all
 // members hold bit-identical scalars and run the same control flow.
+//
+// Two barrier flavours share one arrival counter per image:
+//  * team_sync: bulk data hand-off between members (setup only): every
+//    storing wave drains, agent-scope release before the arrival, agent-scope
+//    acquire after it (cdna_hip_programming.md §6 Guideline 16 recipe);
+//  * the reduction barrier inside team_sum / team_max / team_min: only the
+//    partials cross workgroups, written and read with sc1 (agent-scope
+//    relaxed atomic) accesses, so neither fence is needed.  In the iteration
+//    kernels each member streams only the rows it transforms itself, so the
+//    partials are the only inter-workgroup data.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+typedef __attribute__((address_space(1))) int gi32;
+
 struct Team {
   int m, T;            // member index, team size
   double* part;        // [2][T][kMaxRed] partial slots of this image (double-buffered)
   unsigned int* ctr;   // arrival counter of this image (monotonic across kernels)
   unsigned int base;   // counter value when this kernel started (same in all members)
   int nb;              // team barriers passed in this kernel
-  int* fail;           // set when a barrier spin times out (solve status bit 2)
+  int* fail;           // set when a barrier spin times out (solve status bit 4)
 };
 
-// Work partition of a team: waves (rows / columns) and threads (pixel streams).
+// Work partition of a team.  Waves: row pairs / columns strided by gws from
+// gw0.  Pixel streams: T == 1 streams every pair; T > 1 streams only the
+// chunks of 2*nfw rows (cp pixel pairs) whose row FFTs this member runs, i.e.
+// chunks m, m+T, ...
 struct Part {
   int gw0, gws;  // first global wave index of this workgroup, global wave stride
-  int gt0, gts;  // first global thread index, global thread stride
+  int gt0, gts;  // first global thread index, global thread stride (strided loops)
+  int m, T, cp;  // member, team size, pixel pairs per row chunk
 };
 
-__device__ __forceinline__ Part make_part(const Team& t, int nfw) {
+__device__ __forceinline__ Part make_part(const Team& t, int nfw, int W) {
   Part d;
   d.gw0 = t.m * nfw;
   d.gws = t.T * nfw;
   d.gt0 = t.m * kBlock;
   d.gts = t.T * kBlock;
+  d.m = t.m;
+  d.T = t.T;
+  d.cp = nfw * W;
   return d;
 }
 
@@ -168,14 +203,36 @@ __device__ __forceinline__ Part solo_part(int nfw) {
   d.gws = nfw;
   d.gt0 = 0;
   d.gts = kBlock;
+  d.m = 0;
+  d.T = 1;
+  d.cp = 0;
   return d;
 }
 
-// Team barrier with agent-scope release/acquire (cdna_hip_programming.md §6
-// Guideline 16): every storing wave drains its stores, the workgroup syncs,
-// lane 0 releases, arrives on the counter, polls it relaxed with s_sleep, and
-// acquires; the spin is bounded (timeout sets *fail and lets the kernel end).
-__device__ __forceinline__ void team_barrier(Team& t) {
+// Lane 0: arrive, then wait for all T members (bounded spin with s_sleep;
+// once any barrier of the solve timed out, later ones return at once and the
+// solve ends with status bit 4 instead of hanging).
+__device__ __forceinline__ void team_arrive_wait(Team& t) {
+  __hip_atomic_fetch_add((gu32*)t.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned int target = t.base + (unsigned int)(t.nb + 1) * (unsigned int)t.T;
+  unsigned int spins = 0;
+  while ((int)(__hip_atomic_load((gu32*)t.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+               target) < 0) {
+    __builtin_amdgcn_s_sleep(1);
+    ++spins;
+    if ((spins & 1023u) == 0 &&
+        __hip_atomic_load((gi32*)t.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+      break;
+    if (spins > (1u << 24)) {
+      __hip_atomic_store((gi32*)t.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+}
+
+// Data barrier: everything any member stored before it is visible to every
+// member after it.
+__device__ __forceinline__ void team_sync(Team& t) {
   if (t.T == 1) {
     __syncthreads();
     return;
@@ -185,28 +242,34 @@ __device__ __forceinline__ void team_barrier(Team& t) {
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(t.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned int target = t.base + (unsigned int)(t.nb + 1) * (unsigned int)t.T;
-    unsigned int spins = 0;
-    while ((int)(__hip_atomic_load(t.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) <
-           0) {
-      __builtin_amdgcn_s_sleep(2);
-      ++spins;
-      // once any barrier of the solve timed out, every later one returns at
-      // once: the solve ends quickly with status bit 4 instead of hanging
-      if ((spins & 1023u) == 0 &&
-          __hip_atomic_load(t.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
-        break;
-      if (spins > (1u << 24)) {
-        __hip_atomic_store(t.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
+    team_arrive_wait(t);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
   t.nb += 1;
+}
+
+// Reduction barrier: thread 0 has stored this member's partials with sc1
+// stores; drain them, arrive, wait.  The partials are then read with sc1
+// loads (no acquire needed: nothing else crosses workgroups here).
+__device__ __forceinline__ void team_red_barrier(Team& t) {
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    team_arrive_wait(t);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
+  }
+  __syncthreads();
+  t.nb += 1;
+}
+
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 // Team sum of NV values: every thread of every member gets the totals.
@@ -217,15 +280,26 @@ __device__ __forceinline__ void team_sum(double (&v)[NV], double* red, Team& t) 
   double* slot = t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int i = 0; i < NV; ++i) slot[(size_t)t.m * kMaxRed + i] = v[i];
+    for (int i = 0; i < NV; ++i) st_sc1(slot + (size_t)t.m * kMaxRed + i, v[i]);
   }
-  team_barrier(t);
-  // thread i < NV adds partial i of all members in member order
-  if (threadIdx.x < NV) {
-    const int i = threadIdx.x;
-    double s = 0.0;
-    for (int mm = 0; mm < t.T; ++mm) s += slot[(size_t)mm * kMaxRed + i];
-    red[kWaves * kMaxRed + i] = s;
+  team_red_barrier(t);
+  // wave 0: lane l loads the partials of members l, l+64, ... (all loads in
+  // flight at once), then a fixed shuffle tree: same order in every member
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    double s[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) s[i] = 0.0;
+    for (int mm = lane; mm < t.T; mm += 64) {
+      const double* q = slot + (size_t)mm * kMaxRed;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) s[i] += ld_sc1(q + i);
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const double r = wave_sum(s[i]);
+      if (lane == 0) red[kWaves * kMaxRed + i] = r;
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -239,15 +313,17 @@ __device__ __forceinline__ double team_ext(double v, double* red, Team& t) {
   v = MAX ? block_max(v, red) : block_min(v, red);
   if (t.T == 1) return v;
   double* slot = t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
-  if (threadIdx.x == 0) slot[(size_t)t.m * kMaxRed] = v;
-  team_barrier(t);
-  if (threadIdx.x == 0) {
-    double s = slot[0];
-    for (int mm = 1; mm < t.T; ++mm) {
-      const double u = slot[(size_t)mm * kMaxRed];
+  if (threadIdx.x == 0) st_sc1(slot + (size_t)t.m * kMaxRed, v);
+  team_red_barrier(t);
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    double s = MAX ? -INFINITY : INFINITY;
+    for (int mm = lane; mm < t.T; mm += 64) {
+      const double u = ld_sc1(slot + (size_t)mm * kMaxRed);
       s = MAX ? ((u > s || u != u) ? u : s) : ((u < s || u != u) ? u : s);
     }
-    red[kWaves * kMaxRed] = s;
+    s = MAX ? wave_max(s) : wave_min(s);
+    if (lane == 0) red[kWaves * kMaxRed] = s;
   }
   __syncthreads();
   const double r = red[kWaves * kMaxRed];

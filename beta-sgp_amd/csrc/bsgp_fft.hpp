@@ -52,7 +52,12 @@ struct FftPlan {
   int ns;
   int radix[kMaxStages];
   const cd* tw;  // n entries, exp(-2*pi*i*k/n)
+  int lds_tw;    // device: byte offset of a copy of tw in dynamic LDS, or -1
 };
+
+// Lengths with a compile-time transform (the hot grid sizes: 256 for circular
+// 256^2 images, 270 for 256^2 images with a 25x25 PSF in linear mode).
+BSGP_HD bool fft_static_len(int n) { return n == 256 || n == 270; }
 
 BSGP_HD cd tw_at(const cd* tw, int k, bool inv) {
   cd w = tw[k];
@@ -286,15 +291,29 @@ BSGP_HD cd* fft_run_static(cd* a, cd* b, const cd* tw, bool inv, int lane, int n
   return stages_static<N, 0, 1>(a, b, tw, inv, lane, nlanes, sync);
 }
 
-// Runtime length with compile-time fast paths for the hot grid sizes
-// (256: circular 256^2; 270: 256^2 image with a 25x25 PSF, linear mode).
+// Runtime length with compile-time fast paths for the hot grid sizes.  On the
+// device the static paths read their twiddles from the LDS copy the kernel
+// made (plan.lds_tw >= 0; LDS latency instead of L1/L2 latency in every
+// butterfly round); other lengths read the global table.
+#if defined(__HIP_DEVICE_COMPILE__)
+extern __shared__ __attribute__((aligned(16))) char bsgp_dyn_lds[];
+#endif
 template <class Sync>
 BSGP_HD cd* fft_any(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlanes, Sync sync) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (p.lds_tw >= 0) {
+    const cd* t = reinterpret_cast<const cd*>(bsgp_dyn_lds + p.lds_tw);
+    if (p.n == 256) return fft_run_static<256>(a, b, t, inv, lane, nlanes, sync);
+    return fft_run_static<270>(a, b, t, inv, lane, nlanes, sync);
+  }
+  return fft_run(a, b, p, inv, lane, nlanes, sync);
+#else
   switch (p.n) {
     case 256: return fft_run_static<256>(a, b, p.tw, inv, lane, nlanes, sync);
     case 270: return fft_run_static<270>(a, b, p.tw, inv, lane, nlanes, sync);
     default: return fft_run(a, b, p, inv, lane, nlanes, sync);
   }
+#endif
 }
 
 // Factor n into stage radices: 4s first, then 2, 3, 5, then remaining primes.

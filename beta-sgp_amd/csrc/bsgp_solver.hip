@@ -31,21 +31,32 @@ __device__ __forceinline__ double realtime_s() {
 // U pairs before computing any of them (memory-level parallelism for one
 // workgroup streaming a whole image).  `ld(p)` loads, `cp(p, v)` computes.
 template <int U, class LD, class CP>
-__device__ __forceinline__ void stream2(const Part& D, int npair, LD&& ld, CP&& cp) {
+__device__ __forceinline__ void stream_range(int p0, int p1, LD&& ld, CP&& cp) {
   using T = decltype(ld(0));
-  for (int b = D.gt0 + threadIdx.x; b < npair; b += D.gts * U) {
+  for (int b = p0 + threadIdx.x; b < p1; b += kBlock * U) {
     T v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int p = b + u * D.gts;
-      if (p < npair) v[u] = ld(p);
+      const int p = b + u * kBlock;
+      if (p < p1) v[u] = ld(p);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int p = b + u * D.gts;
-      if (p < npair) cp(p, v[u]);
+      const int p = b + u * kBlock;
+      if (p < p1) cp(p, v[u]);
     }
   }
+}
+// T == 1: the whole image; T > 1: this member's row chunks (Part::cp pairs
+// each), so a pass reads only pixels this member itself produced.
+template <int U, class LD, class CP>
+__device__ __forceinline__ void stream2(const Part& D, int npair, LD&& ld, CP&& cp) {
+  if (D.T == 1) {
+    stream_range<U>(0, npair, ld, cp);
+    return;
+  }
+  for (int p0 = D.m * D.cp; p0 < npair; p0 += D.T * D.cp)
+    stream_range<U>(p0, p0 + D.cp < npair ? p0 + D.cp : npair, ld, cp);
 }
 
 __device__ __forceinline__ double2 ld2(const double* a, int p) {
@@ -175,7 +186,8 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   // counters are zeroed per solve: the setup kernel starts the count at 0
   Team tm = make_team(A, img, st);
   tm.base = 0;
-  const Part D = make_part(tm, G.nfw);
+  const Part D = make_part(tm, G.nfw, G.W);
+  load_tw_lds(G);
   const double* gn_in = A.in.gn + (size_t)img * N;
   const double* bk_in = bmap ? A.in.bkg + (size_t)img * N : nullptr;
   const double bk_scalar_raw = bmap ? 0.0 : A.in.bkg[img];
@@ -254,15 +266,15 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     ProjOut po = project_df_fn(psum, flux, 0.0, 1.0, 1e-11, 0, 0, P.max_projs);
     for (int i = D.gt0 + tid; i < N; i += D.gts) B.xa[i] = clip(B.xa[i], 1.0, po.lam);
   }
-  team_barrier(tm);  // x0 / gns / bks complete before the row passes
+  team_sync(tm);  // x0 / gns / bks complete before the row passes
   // x_tf = A(x), f and g (sgp.py:260-265 / 702-709)
   const double beta0 = A.in.beta0 ? A.in.beta0[img] : P.betaParam;
   Objective obj = make_obj(A, beta0);
   double fsum[3] = {0.0, 0.0, 0.0};  // K, T0, T1
   row_fwd(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.xa[r * G.W + j]; });
-  team_barrier(tm);
+  team_sync(tm);
   col_conv(G, D, B.spec, G.tfA, lds);
-  team_barrier(tm);
+  team_sync(tm);
   const bool beta_obj = P.variant == BSGP_VARIANT_BETA;
   row_inv_fwd(G, D, B.spec, lds, [&](int r, int j, double v) {
     const int i = r * G.W + j;
@@ -276,20 +288,21 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     B.pw[i] = p;
     return g * (p / den);  // gn*den^(b-2) (sgp.py:499)
   });
-  team_sum<3>(fsum, red, tm);  // its barrier publishes xtf / spec
+  team_sum<3>(fsum, red, tm);
+  team_sync(tm);  // publishes xtf / spec / pw
   const double fv = obj.combine(fsum[0], fsum[1], fsum[2], flux, (double)N);
   col_conv(G, D, B.spec, G.tfAT, lds);
-  team_barrier(tm);
+  team_sync(tm);
   row_inv(G, D, B.spec, lds, [&](int r, int j, double at) {
     const int i = r * G.W + j;
     B.ga[i] = (beta_obj ? B.pw[i] : 1.0) - at;  // sgp.py:263 / 499
   });
-  team_barrier(tm);  // every row of spec read before it is overwritten
+  team_sync(tm);  // every row of spec read before it is overwritten
   // scaling-matrix bounds from AT(gn) (sgp.py:268-273)
   row_fwd(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.gns[r * G.W + j]; });
-  team_barrier(tm);
+  team_sync(tm);
   col_conv(G, D, B.spec, G.tfAT, lds);
-  team_barrier(tm);
+  team_sync(tm);
   double ymin = INFINITY, ymax = -INFINITY;
   row_inv(G, D, B.spec, lds, [&](int r, int j, double at) {
     const int i = r * G.W + j;
@@ -354,7 +367,8 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
   if (st.stop) return;
   Team tm = make_team(A, img, st);
   const Geo& G = A.g;
-  const Part Pt = make_part(tm, G.nfw);
+  const Part Pt = make_part(tm, G.nfw, G.W);
+  load_tw_lds(G);
   const bsgp_params& P = A.prm;
   const int N = G.H * G.W;
   const int npair = (N + 1) / 2;
@@ -423,7 +437,8 @@ __global__ void __launch_bounds__(kBlock) k_col(SolveArgs A, int transpose) {
   if (st.stop) return;
   const Team tm = make_team(A, img, st);
   Bufs B = slot_bufs(A, img, 0);
-  col_conv(A.g, make_part(tm, A.g.nfw), B.spec, transpose ? A.g.tfAT : A.g.tfA, lds);
+  load_tw_lds(A.g);
+  col_conv(A.g, make_part(tm, A.g.nfw, A.g.W), B.spec, transpose ? A.g.tfAT : A.g.tfA, lds);
 }
 
 // ------------------------------- kernel: line search + accept + rows of w
@@ -441,7 +456,8 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
   if (st.stop) return;
   Team tm = make_team(A, img, st);
   const Geo& G = A.g;
-  const Part Pt = make_part(tm, G.nfw);
+  const Part Pt = make_part(tm, G.nfw, G.W);
+  load_tw_lds(G);
   const bsgp_params& P = A.prm;
   const int N = G.H * G.W;
   const int npair = (N + 1) / 2;
@@ -672,7 +688,8 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
   if (st.stop) return;
   Team tm = make_team(A, img, st);
   const Geo& G = A.g;
-  const Part Pt = make_part(tm, G.nfw);
+  const Part Pt = make_part(tm, G.nfw, G.W);
+  load_tw_lds(G);
   const bsgp_params& P = A.prm;
   const int N = G.H * G.W;
   const int tid = threadIdx.x;
@@ -803,6 +820,7 @@ __global__ void __launch_bounds__(kBlock) build_tf_kernel(Geo G, const double* k
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cd* lds = reinterpret_cast<cd*>(smem);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  load_tw_lds(G);
   // rows of the P x Q kernel grid -> column-major half spectrum (ld = P)
   row_fwd(G, solo_part(G.nfw), G.P, G.Q, G.P, spec, lds,
           [&](int r, int j) { return kc[r * G.Q + j]; });
@@ -832,6 +850,7 @@ __global__ void __launch_bounds__(kBlock) apply_op_kernel(Geo G, int B, int tran
   cd* lds = reinterpret_cast<cd*>(smem);
   const int N = G.H * G.W;
   cd* spec = specws + (size_t)blockIdx.x * spec_stride;
+  load_tw_lds(G);
   for (int img = blockIdx.x; img < B; img += gridDim.x) {
     const double* xi = x + (size_t)img * N;
     double* oi = out + (size_t)img * N;

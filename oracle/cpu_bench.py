@@ -16,14 +16,30 @@ def gaussian_psf(k, fwhm=None):
     return p / p.sum()
 
 
-def make_stamp(seed, n, k, nstars, bkg=100.0):
+def embed_psf(psf, n):
+    """A k x k PSF placed in an n x n array around (n//2, n//2): the circular
+    A of sgp.py:108-120 needs psf.shape == image shape."""
+    k = psf.shape[0]
+    full = np.zeros((n, n))
+    o = n // 2 - k // 2
+    full[o:o + k, o:o + k] = psf
+    return full / full.sum()
+
+
+def make_stamp(seed, n, k, nstars, bkg=100.0, circular=False):
     from scipy.signal import fftconvolve
     rng = np.random.default_rng(seed)
     obj = np.zeros((n, n))
     p = rng.integers(0, n, (nstars, 2))
     np.add.at(obj, (p[:, 0], p[:, 1]), rng.pareto(1.5, nstars) * 1000 + 100)
     psf = gaussian_psf(k)
-    gn = rng.poisson(np.clip(fftconvolve(obj, psf, mode="same"), 0, None) + bkg).astype(float)
+    if circular:
+        psf = embed_psf(psf, n)
+        tf = np.fft.rfft2(np.fft.fftshift(psf))
+        blurred = np.fft.irfft2(tf * np.fft.rfft2(obj), s=obj.shape)
+    else:
+        blurred = fftconvolve(obj, psf, mode="same")
+    gn = rng.poisson(np.clip(blurred, 0, None) + bkg).astype(float)
     return gn, psf
 
 
@@ -37,7 +53,7 @@ def solve_one(args):
     """One C3-style beta-SGP solve with the oracle; returns (iters, seconds)."""
     seed, n, k, nstars, kw = args
     import sgp_oracle
-    gn, psf = make_stamp(seed, n, k, nstars)
+    gn, psf = make_stamp(seed, n, k, nstars, circular=kw["use_original_SGP_Afunction"])
     t = time.perf_counter()
     _, it, _, _, _ = sgp_oracle.sgp_betaDiv(gn, psf, np.float64(100.0), **kw)
     return it, time.perf_counter() - t

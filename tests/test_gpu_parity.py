@@ -240,3 +240,21 @@ def test_flux_conservation_and_positivity_full_batch(sgpmod):
     assert np.all(out["iters"] == 8)
     d = out["discr"][:, :9]
     assert np.all(np.diff(d, axis=1) <= 1e-9 * np.abs(d[:, 1:]))
+
+
+def test_c4_field_2048_matches_oracle(sgpmod):
+    """BASELINE config C4 geometry: one 2048x2048 field, 64x64 PSF embedded at
+    the centre, circular A (pow-2 FFT), beta-SGP; the numpy oracle on the same
+    inputs (a few iterations keep the CPU side to seconds).  The solve runs
+    as a team of workgroups (team=0 auto for a single image)."""
+    import cpu_bench
+    import sgp_oracle
+    gn, psf = cpu_bench.make_stamp(0, 2048, 64, 5000, circular=True)
+    kw = dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=3, alpha=10.0,
+              ccd_sat_level=65000.0, use_original_SGP_Afunction=True, schedule_lr=True,
+              adapt_beta=False, betaParam=1.05)
+    xr, itr, dr, _, _ = sgp_oracle.sgp_betaDiv(gn, psf, np.float64(100.0), **kw)
+    x, it, d, _, _ = sgpmod.sgp_betaDiv(gn, psf, np.float64(100.0), **kw)
+    assert it == itr
+    assert rel(x, xr) < SOLVE_RTOL, rel(x, xr)
+    np.testing.assert_allclose(d, dr, rtol=1e-7)
