@@ -12,10 +12,13 @@ max-over-ranks wall time of the K timed steps.  Multi-GPU: one process per
 GPU, each rank solves its own batch (seeds offset by rank): weak scaling, no
 collective on the data path.
 
-roofline: algorithmic bytes (8*N*(23 + 2b + 2*E_p + (3+b)*E_ls) per
-image-iteration, E_p/E_ls counted on the device) / average duration of the
-solve kernel measured with HIP events on the launch stream; peak 8.0 TB/s.
-traffic: HBM bytes per launch from a rocprofv3 PMC run (profiles/), if present.
+roofline: algorithmic bytes of the passes the engine makes over HBM-resident
+image vectors (8*N*(23 + 2*proj_passes + 3*ls_passes) per image-iteration plus
+16 B per projection-list entry read, all counted on the device; SURVEY §8d's
+per-evaluation formula is reported beside it) / the solve's duration measured
+with HIP events on the launch stream (the solve is the unit launched: setup +
+MAXIT x five phase kernels on two sub-batch streams); peak 8.0 TB/s.
+traffic: HBM bytes per solve from a rocprofv3 PMC run (profiles/), if present.
 cpu_baseline: the numpy oracle (oracle/sgp_oracle.py, a port of the reference)
 on a bounded sample of the same workload, process pool on this host's cores.
 """
@@ -95,7 +98,7 @@ def synth_batch(B, n, k, nstars, seed0, bkg=100.0, circular=False):
     return gn.contiguous(), psf
 
 
-def solve_kwargs(maxit, ls_spec, streams=None, team=None, circular=False):
+def solve_kwargs(maxit, ls_spec, streams=None, team=None, circular=False, proj_cache=None):
     max_projs, gamma, beta, alpha_min, alpha_max, alpha, M_alpha, tau, M = (
         1000, 1e-4, 0.4, 1e-5, 1e5, 1e1, 3, 0.5, 1)  # sgp.DEFAULT_PARAMS (sgp.py:34)
     return dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=maxit, gamma=gamma, beta=beta,
@@ -103,7 +106,7 @@ def solve_kwargs(maxit, ls_spec, streams=None, team=None, circular=False):
                 M=M, max_projs=max_projs, ccd_sat_level=65000.0, scale_data=True,
                 use_original_SGP_Afunction=circular, adapt_beta=False, betaParam=1.05, lr=1e-3,
                 lr_exp_param=0.1, schedule_lr=True, ls_spec=ls_spec, streams=streams,
-                team=team)
+                team=team, proj_cache=proj_cache)
 
 
 def cpu_baseline(n, k, nstars, images, maxit, workers, circular=False):
@@ -112,9 +115,8 @@ def cpu_baseline(n, k, nstars, images, maxit, workers, circular=False):
     wall time of the solve phase (pool already warm, inputs built in-task)."""
     import cpu_bench
     kw = solve_kwargs(maxit, None, circular=circular)
-    kw.pop("ls_spec")
-    kw.pop("team")
-    kw.pop("streams")
+    for key in ("ls_spec", "team", "streams", "proj_cache"):
+        kw.pop(key)
     iters, wall, cpu_s = cpu_bench.run_pool(n, k, nstars, images, kw, workers)
     return {"value": iters / wall, "unit": "image-iterations/s", "cores": workers,
             "kind": "port",
@@ -166,8 +168,10 @@ def main():
     ap.add_argument("--team", type=int, default=None,
                     help="workgroups per image (0/None = auto, 1 = one per image)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--proj-cache", type=int, default=None)
     ap.add_argument("--cpu-images", type=int, default=16)
-    ap.add_argument("--cpu-maxit", type=int, default=20)
+    ap.add_argument("--cpu-maxit", type=int, default=None,
+                    help="iterations per CPU-baseline image (default: --maxit)")
     args = ap.parse_args()
     global torch
     import torch as _torch
@@ -192,7 +196,8 @@ def main():
     B = args.batch if args.batch else cfg["batch"]
     gn, psf = synth_batch(B, n, k, nstars, seed0=shard_seed0(rank, B), circular=circ)
     bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
-    kw = solve_kwargs(args.maxit, args.ls_spec, args.streams, args.team, circular=circ)
+    kw = solve_kwargs(args.maxit, args.ls_spec, args.streams, args.team, circular=circ,
+                      proj_cache=args.proj_cache)
     torch.cuda.synchronize()
 
     def step():
@@ -225,10 +230,20 @@ def main():
     total_iters = tot * args.steps
     value = total_iters / elapsed_max
 
-    # algorithmic bytes per launch, b = 0 (scalar background)
+    # Algorithmic bytes per solve, b = 0 (scalar background).  SURVEY §8d
+    # prices every projection / line-search *evaluation* as a pass over the
+    # image: 8*N*(23 + 2*E_p + 3*E_ls) per image-iteration.  The engine needs
+    # fewer passes (line-search trials from the moment series, several trials
+    # per pass, projection evaluations from the pixel lists), so the roofline
+    # uses the bytes of the passes it actually makes:
+    #   8*N*(23 + 2*proj_passes + 3*ls_passes) + 16*(list entries read).
     N = n * n
     E_p, E_ls = cnt[:, 0].astype(np.float64), cnt[:, 1].astype(np.float64)
-    alg_bytes = float(np.sum(8.0 * N * (23.0 * iters + 2.0 * E_p + 3.0 * E_ls)))
+    ls_passes = cnt[:, 2].astype(np.float64)
+    proj_passes, list_reads = cnt[:, 6].astype(np.float64), cnt[:, 7].astype(np.float64)
+    survey_bytes = float(np.sum(8.0 * N * (23.0 * iters + 2.0 * E_p + 3.0 * E_ls)))
+    alg_bytes = float(np.sum(8.0 * N * (23.0 * iters + 2.0 * proj_passes + 3.0 * ls_passes)
+                             + 16.0 * list_reads))
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args.config)
     result = {
@@ -252,22 +267,29 @@ def main():
                    "parallelism": f"{world} independent shards (no collective)",
                    "ls_spec": kw["ls_spec"] or sgp.LS_SPEC_DEFAULT,
                    "streams": kw["streams"] or sgp.STREAMS_DEFAULT,
-                   "team": int(cnt[0, 5])},
+                   "team": int(cnt[0, 5]),
+                   "proj_cache": kw["proj_cache"] if kw["proj_cache"] is not None
+                   else sgp.PROJ_CACHE_DEFAULT},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic.get("bytes_per_launch") if traffic else None,
-                     "kernel": "bsgp::sgp_solve_kernel", "kernel_ms": kern_ms,
+                     "kernel": "one solve = setup + MAXIT x (k_dir, k_col, k_ls, k_col, k_bb)",
+                     "kernel_ms": kern_ms,
                      "alg_bytes_per_launch": alg_bytes,
+                     "survey_formula_bytes_per_launch": survey_bytes,
                      "E_p_per_iter": float(E_p.sum() / iters.sum()),
                      "E_ls_per_iter": float(E_ls.sum() / iters.sum()),
-                     "ls_passes_per_iter": float(cnt[:, 2].sum() / iters.sum()),
+                     "proj_passes_per_iter": float(proj_passes.sum() / iters.sum()),
+                     "proj_list_frac_per_iter": float(list_reads.sum() / iters.sum() / N),
+                     "ls_passes_per_iter": float(ls_passes.sum() / iters.sum()),
                      "ls_series_per_iter": float(cnt[:, 4].sum() / iters.sum())},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         workers = max(1, min(16, os.cpu_count() or 1))
         images = args.cpu_images if B > 1 else 1
-        result["cpu_baseline"] = cpu_baseline(n, k, nstars, images, args.cpu_maxit,
+        cpu_maxit = args.cpu_maxit if args.cpu_maxit else args.maxit
+        result["cpu_baseline"] = cpu_baseline(n, k, nstars, images, cpu_maxit,
                                               min(workers, images), circular=circ)
     if rank == 0:
         print(json.dumps(result), flush=True)

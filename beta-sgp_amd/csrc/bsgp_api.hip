@@ -75,10 +75,35 @@ struct bsgp_plan_s {
   size_t tpart_n = 0;
   unsigned int* tctr = nullptr;
   size_t tctr_bytes = 0;
+  // projection pixel lists (proj_cache)
+  double* plist = nullptr;
+  size_t plist_n = 0;
   // operator workspace
   cd* opws = nullptr;
   size_t opws_slots = 0;
 };
+
+// Capacity of one thread's projection list: the pixels it streams in one pass
+// (stream2 in bsgp_solver.hip: T == 1 strides pixel pairs over the block; T > 1
+// strides row chunks of cp = nfw*W pairs over the members).
+static int proj_list_cap(const Geo& g, int T) {
+  const long npair = ((long)g.H * g.W + 1) / 2;
+  if (T == 1) return (int)(2 * ((npair + kBlock - 1) / kBlock));
+  const long cp = (long)g.nfw * g.W;
+  const long nch = (npair + cp - 1) / cp;
+  return (int)(2 * ((nch + T - 1) / T) * ((cp + kBlock - 1) / kBlock));
+}
+
+static int ensure_plist(bsgp_plan p, size_t n) {
+  if (n > p->plist_n) {
+    if (p->plist) HIP_TRY(hipFree(p->plist));
+    p->plist = nullptr;
+    p->plist_n = 0;
+    HIP_TRY(hipMalloc(&p->plist, n * sizeof(double)));
+    p->plist_n = n;
+  }
+  return BSGP_OK;
+}
 
 static int ensure_ws(bsgp_plan p, size_t slots) {
   if (slots > p->ws_slots) {
@@ -340,6 +365,7 @@ int bsgp_plan_destroy(bsgp_plan p) {
   if (p->opws) (void)hipFree(p->opws);
   if (p->tpart) (void)hipFree(p->tpart);
   if (p->tctr) (void)hipFree(p->tctr);
+  if (p->plist) (void)hipFree(p->plist);
   delete p;
   return BSGP_OK;
 }
@@ -402,6 +428,17 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   a.tpart = T > 1 ? p->tpart : nullptr;
   a.tctr = p->tctr;
   a.tfail = reinterpret_cast<int*>(p->tctr + B);
+  a.plist = nullptr;
+  a.plist_stride = 0;
+  a.lcap = 0;
+  if (prm->proj_cache && prm->proj_type == 1) {
+    a.lcap = proj_list_cap(p->g, T);
+    const size_t half = round_up((size_t)a.lcap * T * kBlock, 32);
+    a.plist_stride = 2 * half;
+    rc = ensure_plist(p, (size_t)B * a.plist_stride);
+    if (rc) return rc;
+    a.plist = p->plist;
+  }
   hipStream_t s = (hipStream_t)stream;
   const int K = (prm->adapt_beta && prm->variant == BSGP_VARIANT_BETA)
                     ? 1

@@ -549,126 +549,162 @@ __device__ __forceinline__ double proj_sum(int N, CDF& cdf, const ProjClip& clip
   return s[0];
 }
 
+// The reference's multiplier search as a stepper: `lam` is the multiplier
+// whose sum is wanted next; feed(sum_i x_i(lam)) advances the search and
+// returns false once it has finished (result in `lam`).  One evaluation site
+// in the caller's loop keeps the (large, fused) evaluation code inlined once.
+//   phase 0: first evaluation (:22-28)
+//   phase 1: r < 0 bracketing loop (:30-53)
+//   phase 2: r > 0 bracketing loop (:55-81), with the np.errstate overflow break
+//   phase 3: secant loop (:96-142), including the :122 slip (x assigned, not s)
+struct ProjDF {
+  static constexpr int kCap = 200000;  // hard bound: the reference's r<0 bracket can spin forever
+  double b, tol_r, tol_lam;
+  double lam, dlam, laml, lamu, rl, ru, s, r;
+  int biter, siter, nev, maxit_s, max_projs, phase;
+
+  __device__ __forceinline__ void init(double b_, double lambda_, double dlambda_, double tol_lam_,
+                                       int biter_, int siter_, int max_projs_) {
+    b = b_;
+    tol_r = 1e-11 * b_;
+    tol_lam = tol_lam_;
+    lam = lambda_;
+    dlam = dlambda_;
+    laml = lamu = rl = ru = s = r = 0.0;
+    biter = biter_;
+    siter = siter_;
+    max_projs = max_projs_;
+    maxit_s = 0;
+    nev = 0;
+    phase = 0;
+  }
+  __device__ __forceinline__ bool finish(double l) {
+    lam = l;
+    phase = 4;
+    return false;
+  }
+  __device__ __forceinline__ bool secant_start() {
+    if (fabs(ru) < tol_r) return finish(lamu);  // :84-88
+    if (fabs(rl) < tol_r) return finish(laml);  // :89-93
+    s = 1 - rl / ru;                            // :96-102
+    dlam = dlam / s;
+    lam = lamu - dlam;
+    maxit_s = max_projs - biter;
+    phase = 3;
+    return true;
+  }
+  __device__ __forceinline__ bool feed(double S) {
+    r = S - b;
+    ++nev;
+    if (phase == 0) {
+      if (fabs(r) < tol_r) return finish(lam);
+      if (r < 0) {
+        laml = lam;
+        rl = r;
+        lam = lam + dlam;
+        phase = 1;
+      } else {
+        lamu = lam;
+        ru = r;
+        lam = lam - dlam;
+        phase = 2;
+      }
+      return true;
+    }
+    if (phase == 1) {
+      if (r < 0 && nev < kCap) {
+        biter = biter + 1;
+        laml = lam;
+        s = np_max2(rl / r - 1, 0.1);
+        dlam = dlam + dlam / s;
+        lam = lam + dlam;
+        rl = r;
+        return true;
+      }
+      lamu = lam;
+      ru = r;
+      return secant_start();
+    }
+    if (phase == 2) {
+      if (r > 0 && nev < kCap) {
+        biter = biter + 1;
+        lamu = lam;
+        s = np_max2(ru / r - 1, 0.1);
+        // np.errstate(all='raise') around dlambda_ + dlambda_/s: overflow -> break
+        const double q = dlam / s;
+        const double nd = dlam + q;
+        const bool fin_in = isfinite(dlam) && isfinite(s);
+        if (!(fin_in && (!isfinite(q) || !isfinite(nd) || s == 0.0))) {
+          dlam = nd;
+          lam = lam - dlam;
+          ru = r;
+          return true;
+        }
+      }
+      laml = lam;
+      rl = r;
+      return secant_start();
+    }
+    // phase 3: loop condition, then one secant step
+    if (!(fabs(r) > tol_r && dlam > tol_lam * (1 + fabs(lam)) && siter < maxit_s && nev < kCap))
+      return finish(lam);
+    siter = siter + 1;
+    if (r > 0) {
+      if (s <= 2) {
+        lamu = lam;
+        ru = r;
+        s = 1 - rl / ru;
+        dlam = (lamu - laml) / s;
+        lam = lamu - dlam;
+      } else {
+        s = np_max2(ru / r - 1, 0.1);
+        dlam = (lamu - lam) / s;
+        const double lam_new = np_max2(lam - dlam, 0.75 * laml + 0.25 * lam);
+        lamu = lam;
+        ru = r;
+        lam = lam_new;
+        // flux_conserve_proj.py:122 assigns x, not s: s keeps the value above
+      }
+    } else {
+      if (s >= 2) {
+        laml = lam;
+        rl = r;
+        s = 1 - rl / ru;
+        dlam = (lamu - laml) / s;
+        lam = lamu - dlam;
+      } else {
+        s = np_max2(rl / r - 1, 0.1);
+        dlam = (lam - laml) / s;
+        const double lam_new = np_min2(lam + dlam, 0.75 * lamu + 0.25 * lam);
+        laml = lam;
+        rl = r;
+        lam = lam_new;
+        s = (lamu - laml) / (lamu - lam);
+      }
+    }
+    return true;
+  }
+  __device__ __forceinline__ ProjOut out() const {
+    ProjOut o;
+    o.lam = lam;
+    o.evals = nev;
+    o.biter = biter;
+    o.siter = siter;
+    return o;
+  }
+};
+
 // `sumf(lambda)` returns sum_i x_i(lambda) over the image (a workgroup
 // reduction); every thread runs the identical scalar search.
 template <class SUMF>
 __device__ __forceinline__ ProjOut project_df_fn(SUMF&& sumf, double b, double lambda_,
                                                  double dlambda_, double tol_lam, int biter,
                                                  int siter, int max_projs) {
-  const int kCap = 200000;  // hard bound: the reference's r<0 bracket can spin forever
-  ProjOut o;
-  int nev = 0;
-  const double tol_r = 1e-11 * b;
-  double r = sumf(lambda_) - b;
-  ++nev;
-  double lambdal = 0, lambdau = 0, rl = 0, ru = 0, s = 0;
-  if (fabs(r) < tol_r) goto done;
-  if (r < 0) {
-    lambdal = lambda_;
-    rl = r;
-    lambda_ = lambda_ + dlambda_;
-    r = sumf(lambda_) - b;
-    ++nev;
-    while (r < 0 && nev < kCap) {
-      biter = biter + 1;
-      lambdal = lambda_;
-      s = np_max2(rl / r - 1, 0.1);
-      dlambda_ = dlambda_ + dlambda_ / s;
-      lambda_ = lambda_ + dlambda_;
-      rl = r;
-      r = sumf(lambda_) - b;
-      ++nev;
-    }
-    lambdau = lambda_;
-    ru = r;
-  } else {
-    lambdau = lambda_;
-    ru = r;
-    lambda_ = lambda_ - dlambda_;
-    r = sumf(lambda_) - b;
-    ++nev;
-    while (r > 0 && nev < kCap) {
-      biter = biter + 1;
-      lambdau = lambda_;
-      s = np_max2(ru / r - 1, 0.1);
-      // np.errstate(all='raise') around dlambda_ + dlambda_/s: overflow -> break
-      {
-        const double q = dlambda_ / s;
-        const double nd = dlambda_ + q;
-        const bool fin_in = isfinite(dlambda_) && isfinite(s);
-        if (fin_in && (!isfinite(q) || !isfinite(nd))) break;
-        if (fin_in && s == 0.0) break;
-        dlambda_ = nd;
-      }
-      lambda_ = lambda_ - dlambda_;
-      ru = r;
-      r = sumf(lambda_) - b;
-      ++nev;
-    }
-    lambdal = lambda_;
-    rl = r;
+  ProjDF pd;
+  pd.init(b, lambda_, dlambda_, tol_lam, biter, siter, max_projs);
+  while (pd.feed(sumf(pd.lam))) {
   }
-  if (fabs(ru) < tol_r) {
-    lambda_ = lambdau;
-    goto done;
-  }
-  if (fabs(rl) < tol_r) {
-    lambda_ = lambdal;
-    goto done;
-  }
-  s = 1 - rl / ru;
-  dlambda_ = dlambda_ / s;
-  lambda_ = lambdau - dlambda_;
-  r = sumf(lambda_) - b;
-  ++nev;
-  {
-    const int maxit_s = max_projs - biter;
-    while (fabs(r) > tol_r && dlambda_ > tol_lam * (1 + fabs(lambda_)) && siter < maxit_s &&
-           nev < kCap) {
-      siter = siter + 1;
-      if (r > 0) {
-        if (s <= 2) {
-          lambdau = lambda_;
-          ru = r;
-          s = 1 - rl / ru;
-          dlambda_ = (lambdau - lambdal) / s;
-          lambda_ = lambdau - dlambda_;
-        } else {
-          s = np_max2(ru / r - 1, 0.1);
-          dlambda_ = (lambdau - lambda_) / s;
-          const double lambda_new = np_max2(lambda_ - dlambda_, 0.75 * lambdal + 0.25 * lambda_);
-          lambdau = lambda_;
-          ru = r;
-          lambda_ = lambda_new;
-          // flux_conserve_proj.py:122 assigns x, not s: s keeps the value above
-        }
-      } else {
-        if (s >= 2) {
-          lambdal = lambda_;
-          rl = r;
-          s = 1 - rl / ru;
-          dlambda_ = (lambdau - lambdal) / s;
-          lambda_ = lambdau - dlambda_;
-        } else {
-          s = np_max2(rl / r - 1, 0.1);
-          dlambda_ = (lambda_ - lambdal) / s;
-          const double lambda_new = np_min2(lambda_ + dlambda_, 0.75 * lambdau + 0.25 * lambda_);
-          lambdal = lambda_;
-          rl = r;
-          lambda_ = lambda_new;
-          s = (lambdau - lambdal) / (lambdau - lambda_);
-        }
-      }
-      r = sumf(lambda_) - b;
-      ++nev;
-    }
-  }
-done:
-  o.lam = lambda_;
-  o.evals = nev;
-  o.biter = biter;
-  o.siter = siter;
-  return o;
+  return pd.out();
 }
 
 

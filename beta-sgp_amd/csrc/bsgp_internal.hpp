@@ -14,6 +14,7 @@ struct ImgState {
   int par, Xones, stop, iter, epoch;
   int bar_base;  // team-barrier counter value at the start of the next kernel (T > 1)
   int64_t E_p, E_ls, ls_passes, status, ls_series;
+  int64_t proj_passes, proj_list;  // projection passes over the image / list entries read
   double sc, flux, bks_scalar, lo, hi, Dcoeff, tol, t0;
   double fv, alpha, tau, lr, init_lr, beta, lam_p, gd, lam;
   double konst;  // lambda-independent objective sum at `beta` (sum s*gn^b / sum gn)
@@ -41,6 +42,11 @@ struct SolveArgs {
   double* tpart;        // [B][2][T][kMaxRed] reduction partials
   unsigned int* tctr;   // [B] barrier arrival counters, zeroed per solve
   int* tfail;           // set by a timed-out barrier spin
+  // projection pixel lists (proj_cache): per image two arrays (y, X) of
+  // lcap * T * kBlock doubles; entry k of global thread gt at k*T*kBlock + gt
+  double* plist;
+  size_t plist_stride;  // doubles per image (both arrays)
+  int lcap;             // list capacity per thread (pixels one thread streams)
 };
 
 hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s);

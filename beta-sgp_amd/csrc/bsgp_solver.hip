@@ -106,6 +106,21 @@ struct Dir {
     c = y * D;
     dia = D;
   }
+  // y = x - alpha*X*g and X of one pixel (sgp.py:311-313)
+  __device__ __forceinline__ void yx(double x, double g, double& y, double& X) const {
+    X = Xones ? 1.0 : clipX(x, lo, hi);
+    y = x - alpha * (X * g);
+  }
+  // x_i(lambda) of projectDF(flux, y*D, D) in multiplier form: (c + lam)/dia
+  // = y + lam*X up to rounding, clipped to [0, sat] (flux_conserve_proj.py:22-25).
+  // The sums of the multiplier search use this form; the projected pixels
+  // themselves (d below) use the reference's division.
+  __device__ __forceinline__ double pv(double y, double X, double lam) const {
+    double v = fma(lam, X, y);
+    v = (0.0 > v) ? 0.0 : v;
+    if (clip.has_sat) v = (clip.satv < v) ? clip.satv : v;
+    return v;
+  }
   __device__ __forceinline__ double d(double x, double g) const {
     double y;
     if (proj) {
@@ -337,6 +352,8 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     st.epoch = 0;
     st.bar_base = (int)((unsigned int)tm.T * (unsigned int)tm.nb);
     st.E_p = st.E_ls = st.ls_passes = st.status = st.ls_series = 0;
+    st.proj_passes = st.proj_list = 0;
+    st.lam_p = 0.0;  // no previous multiplier: the first projection splits no bracket
     st.sc = sc;
     st.flux = flux;
     st.bks_scalar = bks_scalar;
@@ -354,6 +371,194 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     st.konst = fsum[0];
     atomicAdd(A.active, 1);
   }
+}
+
+// --------------------------------------- projection with pixel lists
+// projectDF(flux, y*D, D) (flux_conserve_proj.py:7-144) for the direction of
+// sgp.py:311-318: the reference's multiplier sequence, step for step
+// (project_df_fn).  What changes is how sum_i x_i(lambda) is evaluated:
+//  * the first evaluation (lambda_ = 0) is a full pass over (x, g) that also
+//    sums x(lambda_ - dlambda_) and x(lambda_ + dlambda_), the second
+//    evaluation of either bracketing branch (:32 / :57), and the slope at
+//    lambda_ (for a Newton bound on the root);
+//  * a full pass can split the pixels for a bracket [qL, qU]: pixels at 0 or
+//    at saturation for every lambda in it add a constant, pixels strictly
+//    inside add y + lambda*X (two running sums), and only the pixels that
+//    change state inside the bracket go to this thread's list (y, X);
+//  * an evaluation whose lambda lies in the split bracket reads only the list
+//    (typically 2-5% of the pixels, written and read back by the same thread).
+// Split brackets: the previous iteration's multiplier +/- 30% on the first
+// pass; on the first miss, the hull of the missing lambda and the Newton
+// bound (for the convex sum the secant and Newton iterates fall on either
+// side of the root); on later misses, the tightest bracket of signs seen.
+// A miss is just a full pass, so the choice of bracket never changes results.
+constexpr double kProjGuessW = 0.3;
+
+__device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt, Team& tm,
+                                     const Dir& D, const Bufs& B, double* red, double lam_prev,
+                                     double flux, int npair, bool odd, int N, int64_t& passes,
+                                     int64_t& list_reads) {
+  const double* xa = B.xa;
+  const double* ga = B.ga;
+  const int LS = tm.T * kBlock;
+  const int gt = tm.m * kBlock + (int)threadIdx.x;
+  double* ly = A.plist + (size_t)img * A.plist_stride;
+  double* lX = ly + A.plist_stride / 2;
+  const int lcap = A.lcap;
+  const bool hs = D.clip.has_sat;
+  const double satv = D.clip.satv;
+  // identical in every thread of the team
+  bool have = false;
+  double cL = 0.0, cU = 0.0, SA = 0.0, SB = 0.0, nsat = 0.0, nstr = 0.0;
+  double Lk = -INFINITY, Uk = INFINITY;  // largest lambda with r < 0, smallest with r > 0
+  double xl0 = NAN, xs0 = 0.0, xl1 = NAN, xs1 = 0.0, lamN = NAN;
+  bool first_miss = true;
+  int calls = 0;
+  int cnt = 0;  // this thread's list entries
+
+  auto note = [&](double lam, double S) {
+    const double r = S - flux;
+    if (r < 0 && lam > Lk) Lk = lam;
+    if (r > 0 && lam < Uk) Uk = lam;
+  };
+  // One full pass: sums at lams[0..NL), optional split for [qL, qU]; returns
+  // the slope sum_{0 < x_i(lams[0]) < sat} X_i.
+  auto pass = [&](auto nlc, const double* lams, double* S, bool split, double qL,
+                  double qU) -> double {
+    constexpr int NL = decltype(nlc)::value;
+    constexpr int NT = NL + 6;  // sums | SA, SB, n_sat, n_list, n_overflow | slope
+    double t[NT];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) t[k] = 0.0;
+    double lm[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) lm[k] = lams[k];
+    if (split) cnt = 0;
+    auto px = [&](double x, double g) __attribute__((always_inline)) {
+      double y, X;
+      D.yx(x, g, y, X);
+#pragma unroll
+      for (int k = 0; k < NL; ++k) {
+        const double v = D.pv(y, X, lm[k]);
+        t[k] += v;
+        if (k == 0 && v > 0.0 && (!hs || v < satv)) t[NL + 5] += X;
+      }
+      if (split) {
+        const double vL = D.pv(y, X, qL), vU = D.pv(y, X, qU);
+        if (vU == 0.0) {
+          // 0 for every lambda <= qU
+        } else if (hs && vL == satv) {
+          t[NL + 2] += 1.0;  // saturated for every lambda >= qL
+        } else if (vL > 0.0 && (!hs || vU < satv)) {
+          t[NL] += y;  // unclipped over the whole bracket
+          t[NL + 1] += X;
+        } else if (cnt < lcap) {
+          ly[(size_t)cnt * LS + gt] = y;
+          lX[(size_t)cnt * LS + gt] = X;
+          ++cnt;
+          t[NL + 3] += 1.0;
+        } else {
+          t[NL + 4] += 1.0;
+        }
+      }
+    };
+    stream2<4>(
+        Pt, npair,
+        [&](int p) {
+          struct V {
+            double2 x, g;
+          } v;
+          v.x = ld2(xa, p);
+          v.g = ld2(ga, p);
+          return v;
+        },
+        [&](int p, const auto& v) {
+          px(v.x.x, v.g.x);
+          if (!odd || 2 * p + 1 < N) px(v.x.y, v.g.y);
+        });
+    // the list is read back by the thread that wrote it: drain its stores
+    if (split) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    team_sum<NT>(t, red, tm);
+#pragma unroll
+    for (int k = 0; k < NL; ++k) S[k] = t[k];
+    if (split) {
+      have = t[NL + 4] == 0.0;
+      cL = qL;
+      cU = qU;
+      SA = t[NL];
+      SB = t[NL + 1];
+      nsat = t[NL + 2];
+      nstr = t[NL + 3];
+    }
+    ++passes;
+    return t[NL + 5];
+  };
+  // sum over the split bracket's list
+  auto leval = [&](double lam) {
+    double t[1] = {0.0};
+    int k = 0;
+    for (; k + 4 <= cnt; k += 4) {
+      double yv[4], Xv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        yv[u] = ly[(size_t)(k + u) * LS + gt];
+        Xv[u] = lX[(size_t)(k + u) * LS + gt];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[0] += D.pv(yv[u], Xv[u], lam);
+    }
+    for (; k < cnt; ++k) t[0] += D.pv(ly[(size_t)k * LS + gt], lX[(size_t)k * LS + gt], lam);
+    team_sum<1>(t, red, tm);
+    const double lin = SA + lam * SB;
+    return (hs ? lin + nsat * satv : lin) + t[0];
+  };
+  auto sumf = [&](double lam) {
+    double S;
+    if (calls == 0) {
+      const double lams[3] = {lam, lam - 1.0, lam + 1.0};  // lambda_ -/+ dlambda_ (dlambda_ = 1)
+      double Sv[3];
+      const bool guess = isfinite(lam_prev) && lam_prev != 0.0;
+      const double w = kProjGuessW * fabs(lam_prev);
+      const double slope = pass(std::integral_constant<int, 3>{}, lams, Sv, guess,
+                                lam_prev - w, lam_prev + w);
+      S = Sv[0];
+      xl0 = lams[1];
+      xs0 = Sv[1];
+      xl1 = lams[2];
+      xs1 = Sv[2];
+      note(lams[1], Sv[1]);
+      note(lams[2], Sv[2]);
+      lamN = slope > 0.0 ? lam - (S - flux) / slope : NAN;
+    } else if (lam == xl0) {
+      S = xs0;
+    } else if (lam == xl1) {
+      S = xs1;
+    } else if (have && lam >= cL && lam <= cU) {
+      S = leval(lam);
+      list_reads += (int64_t)nstr;
+    } else {
+      bool split = false;
+      double qL = 0.0, qU = 0.0;
+      if (first_miss && isfinite(lamN)) {
+        qL = fmin(lam, lamN);
+        qU = fmax(lam, lamN);
+        split = true;
+      } else if (isfinite(Lk) && isfinite(Uk)) {
+        qL = fmin(Lk, Uk);
+        qU = fmax(Lk, Uk);
+        split = true;
+      }
+      first_miss = false;
+      const double lams[1] = {lam};
+      double Sv[1];
+      (void)pass(std::integral_constant<int, 1>{}, lams, Sv, split, qL, qU);
+      S = Sv[0];
+    }
+    ++calls;
+    note(lam, S);
+    return S;
+  };
+  return project_df_fn(sumf, flux, 0.0, 1.0, 1e-11, 0, 0, A.prm.max_projs);
 }
 
 // ------------------------------------------ kernel: direction + rows of d
@@ -377,7 +582,13 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
   Dir D = make_dir(A, st);
   const double flux = st.flux;
   int evals = 0;
-  if (P.proj_type == 1) {
+  int64_t ppass = 0, plist_reads = 0;
+  if (P.proj_type == 1 && A.plist != nullptr) {
+    ProjOut po = cached_projection(A, img, Pt, tm, D, B, red, st.lam_p, flux, npair, odd, N,
+                                   ppass, plist_reads);
+    D.lam_p = po.lam;
+    evals = po.evals;
+  } else if (P.proj_type == 1) {
     const double* xa = B.xa;
     const double* ga = B.ga;
     auto psum = [&](double lam) {
@@ -407,6 +618,7 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
     ProjOut po = project_df_fn(psum, flux, 0.0, 1.0, 1e-11, 0, 0, P.max_projs);
     D.lam_p = po.lam;
     evals = po.evals;
+    ppass = po.evals;
   }
   double gd[1] = {0.0};
   row_fwd(G, Pt, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) {
@@ -425,6 +637,8 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
     st.epoch += 1;
     st.lam_p = D.lam_p;
     st.E_p += evals;
+    st.proj_passes += ppass;
+    st.proj_list += plist_reads;
     st.gd = gd[0];
   }
 }
@@ -806,7 +1020,8 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
                                               __HIP_MEMORY_SCOPE_AGENT)) ? 4 : 0);
         c[4] = st.ls_series;
         c[5] = tm.T;
-        c[6] = c[7] = 0;
+        c[6] = st.proj_passes;
+        c[7] = st.proj_list;
       }
       atomicSub(A.active, 1);
     }

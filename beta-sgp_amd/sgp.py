@@ -47,6 +47,7 @@ LS_SPEC_DEFAULT = 2  # line-search trial lambdas evaluated per pass over the dat
 LS_SERIES_DEFAULT = 1  # small line-search steps from the moment series (general beta)
 STREAMS_DEFAULT = 2  # sub-batch streams of a batched solve
 TEAM_DEFAULT = 0  # workgroups per image: 0 = auto (spread small batches over the CUs)
+PROJ_CACHE_DEFAULT = 1  # projectDF evaluations inside a known root bracket read a pixel list
 
 
 # ------------------------------------------------------------------ helpers
@@ -100,7 +101,7 @@ def _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, 
             alpha_max, M_alpha, tau, M, max_projs, verbose, ccd_sat_level, scale_data,
             tol_convergence, adapt_beta=False, betaParam=1.005, lr=1e-3, lr_exp_param=0.1,
             schedule_lr=False, bkg_is_map=False, ls_spec=None, ls_series=None, streams=None,
-            team=None):
+            team=None, proj_cache=None):
     p = _B.Params()
     p.variant = variant
     p.init_recon = int(init_recon)
@@ -126,6 +127,7 @@ def _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, 
     p.ls_series = LS_SERIES_DEFAULT if ls_series is None else int(bool(ls_series))
     p.streams = STREAMS_DEFAULT if streams is None else int(streams)
     p.team = TEAM_DEFAULT if team is None else int(team)
+    p.proj_cache = PROJ_CACHE_DEFAULT if proj_cache is None else int(bool(proj_cache))
     return p
 
 
@@ -298,7 +300,7 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
                  ccd_sat_level=None, scale_data=True, tol_convergence=1e-4,
                  use_original_SGP_Afunction=True, adapt_beta=False, betaParam=1.005, lr=1e-3,
                  lr_exp_param=0.1, schedule_lr=False, ls_spec=None, ls_series=None,
-                 streams=None, team=None, device_out=False):
+                 streams=None, team=None, proj_cache=None, device_out=False):
     _check_psf(np.asarray(psf))
     torch = _B.torch
     _B.require_gpu()
@@ -316,7 +318,7 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
                   scale_data, tol_convergence, adapt_beta=adapt_beta, betaParam=betaParam, lr=lr,
                   lr_exp_param=lr_exp_param, schedule_lr=schedule_lr, bkg_is_map=bkg_is_map,
                   ls_spec=ls_spec, ls_series=ls_series, streams=streams,
-                  team=team)
+                  team=team, proj_cache=proj_cache)
     x0 = None
     if init_recon == 1:
         np.random.seed(42)

@@ -80,6 +80,10 @@ typedef struct {
   int32_t team;           /* workgroups cooperating on one image: 0 = auto (spread the
                              batch over the CUs when B is small), 1 = one per image,
                              k > 1 = at most k (capped so every workgroup is resident) */
+  int32_t proj_cache;     /* 1: projectDF evaluations whose multiplier falls inside a
+                             bracket known to hold the root read only the pixels that
+                             change state inside it (a per-lane list written by the
+                             last full pass); 0: every evaluation streams the image */
 } bsgp_params;
 
 /* Device inputs of a batched solve. */
@@ -103,7 +107,8 @@ typedef struct {
   int64_t* counters;   /* [B][8]: proj evals E_p, line-search trials E_ls,
                           line-search passes over the image, status bits (1: line
                           search cap, 4: team barrier timed out), trials evaluated
-                          from the small-step series, team size T, 2 reserved;
+                          from the small-step series, team size T, projection
+                          passes over the image, projection-list entries read;
                           may be NULL */
 } bsgp_outputs;
 
