@@ -377,75 +377,150 @@ __device__ __forceinline__ void store_pair(cd* col, bool two, bool pair_ok, cd a
   }
 }
 
-// row_fwd: for every pair of image rows (r, r+1) one wave FFTs z = a + i b
+// Memory-level parallelism of the row and column passes: every global load a
+// wave needs for one row pair (or column) is issued before any of it is
+// used, so a row pair costs about one memory round trip instead of one per
+// 64-pixel step.  Operand loads go through a loader lambda `ld(r, j) -> V`
+// that only loads; the lambda that uses them (and may store) runs after the
+// whole batch is in registers.
+constexpr int kJCH = 4;  // pixels per lane per row in one load batch (W <= 256: one batch)
+constexpr int kGCH = 3;  // stored spectrum columns per lane in one gather batch (Qh <= 192)
+constexpr int kPCH = 5;  // column elements per lane in one batch (P <= 320: one batch)
+
+// Issue the loads of one batch of row pixels j0 + lane + 64u (u < kJCH) of
+// rows r and r+1.
+template <int JCH, class LD, class V>
+__device__ __forceinline__ void load_rows(LD& ld, int r, bool two, int j0, int lane, int ncols,
+                                          V (&v0)[JCH], V (&v1)[JCH]) {
+#pragma unroll
+  for (int u = 0; u < JCH; ++u) {
+    const int j = j0 + lane + 64 * u;
+    if (j < ncols) {
+      v0[u] = ld(r, j);
+      if (two) v1[u] = ld(r + 1, j);
+    }
+  }
+}
+
+// row_fwd2: for every pair of image rows (r, r+1) one wave FFTs z = a + i b
 // (a, b real rows of length ncols zero-padded to Q) and stores the two half
 // spectra into column-major spec with leading dimension ld (>= nrows).
-// `prod(r, j)` produces the real input pixel (fused producer).
-template <class Prod>
-__device__ __forceinline__ void row_fwd(const Geo& G, const Part& D, int nrows, int ncols, int ld,
-                                        cd* spec, cd* lds, Prod&& prod) {
+// The input pixel is mk(r, j, ld(r, j)) (fused producer).
+template <int JCH = kJCH, class LD, class MK>
+__device__ __forceinline__ void row_fwd2(const Geo& G, const Part& D, int nrows, int ncols,
+                                         int ldim, cd* spec, cd* lds, LD&& ld, MK&& mk) {
+  using V = decltype(ld(0, 0));
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bool pair_ok = (ld & 1) == 0;
+  const bool pair_ok = (ldim & 1) == 0;
   if (w < G.nfw) {
     cd* a = lds + w * 2 * G.lpad;
     cd* b = a + G.lpad;
     for (int r = 2 * (D.gw0 + w); r < nrows; r += 2 * D.gws) {
       const bool two = (r + 1) < nrows;
-      for (int j = lane; j < G.Q; j += 64) {
-        double va = 0.0, vb = 0.0;
-        if (j < ncols) {
-          va = prod(r, j);
-          if (two) vb = prod(r + 1, j);
+      for (int j0 = 0; j0 < G.Q; j0 += 64 * JCH) {
+        V v0[JCH], v1[JCH];
+        load_rows<JCH>(ld, r, two, j0, lane, ncols, v0, v1);
+#pragma unroll
+        for (int u = 0; u < JCH; ++u) {
+          const int j = j0 + lane + 64 * u;
+          if (j < G.Q) {
+            double va = 0.0, vb = 0.0;
+            if (j < ncols) {
+              va = mk(r, j, v0[u]);
+              if (two) vb = mk(r + 1, j, v1[u]);
+            }
+            a[j] = cmk(va, vb);
+          }
         }
-        a[j] = cmk(va, vb);
       }
       wave_sync();
       cd* Z = fft_any(a, b, G.fq, false, lane, 64, WaveSync());
       for (int k = lane; k < G.Qh; k += 64) {
         cd ak, bk;
         r2c_split(Z, G.Q, k, &ak, &bk);
-        store_pair(spec + (size_t)k * ld + r, two, pair_ok, ak, bk);
+        store_pair(spec + (size_t)k * ldim + r, two, pair_ok, ak, bk);
       }
       wave_sync();
     }
   }
 }
 
-// Rebuild the full-length spectrum of row pair (r, r+1) into `a`.
+// row_fwd: producer form, `prod(r, j)` returns the input pixel.
+template <class Prod>
+__device__ __forceinline__ void row_fwd(const Geo& G, const Part& D, int nrows, int ncols, int ldim,
+                                        cd* spec, cd* lds, Prod&& prod) {
+  row_fwd2(G, D, nrows, ncols, ldim, spec, lds, prod, [](int, int, double v) { return v; });
+}
+
+// Rebuild the full-length spectrum of row pair (r, r+1) into `a`: each
+// stored column k < Qh is loaded once and yields Z_k and Z_{Q-k}.
 __device__ __forceinline__ void gather_pair(const Geo& G, const cd* spec, int ld, int r, bool two,
                                             cd* a, int lane) {
-  for (int k = lane; k < G.Q; k += 64) {
-    const bool lo = k < G.Qh;
-    const cd* col = spec + (size_t)(lo ? k : G.Q - k) * ld + r;
-    const cd A = col[0];
-    const cd B = two ? col[1] : cmk(0.0, 0.0);
-    a[k] = lo ? cmk(A.x - B.y, A.y + B.x) : cmk(A.x + B.y, B.x - A.y);
+  for (int k0 = lane; k0 < G.Qh; k0 += 64 * kGCH) {
+    cd A[kGCH], B[kGCH];
+#pragma unroll
+    for (int u = 0; u < kGCH; ++u) {
+      const int k = k0 + 64 * u;
+      if (k < G.Qh) {
+        const cd* col = spec + (size_t)k * ld + r;
+        A[u] = col[0];
+        B[u] = two ? col[1] : cmk(0.0, 0.0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kGCH; ++u) {
+      const int k = k0 + 64 * u;
+      if (k < G.Qh) {
+        a[k] = cmk(A[u].x - B[u].y, A[u].y + B[u].x);
+        if (k > 0 && G.Q - k >= G.Qh) a[G.Q - k] = cmk(A[u].x + B[u].y, B[u].x - A[u].y);
+      }
+    }
   }
 }
 
-// row_inv: inverse row transforms; `cons(r, j, value)` consumes each output
-// pixel (j < W) of rows [0, H).  The 1/(P*Q) scale is folded into the TF.
-template <class Cons>
-__device__ __forceinline__ void row_inv(const Geo& G, const Part& D, const cd* spec, cd* lds,
-                                        Cons&& cons) {
+// row_inv2: inverse row transforms; use(r, j, value, ld(r, j)) consumes each
+// output pixel (j < W) of rows [0, H).  The 1/(P*Q) scale is folded into the
+// TF.  PRE: the first operand batch is issued before the spectrum gather, so
+// its latency hides under the gather and the FFT (costs its registers across
+// the FFT).
+template <bool PRE, int JCH = kJCH, class LD, class USE>
+__device__ __forceinline__ void row_inv2(const Geo& G, const Part& D, const cd* spec, cd* lds,
+                                         LD&& ld, USE&& use) {
+  using V = decltype(ld(0, 0));
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (w < G.nfw) {
     cd* a = lds + w * 2 * G.lpad;
     cd* b = a + G.lpad;
     for (int r = 2 * (D.gw0 + w); r < G.H; r += 2 * D.gws) {
       const bool two = (r + 1) < G.H;
+      V v0[JCH], v1[JCH];
+      if (PRE) load_rows<JCH>(ld, r, two, 0, lane, G.W, v0, v1);
       gather_pair(G, spec, G.H, r, two, a, lane);
       wave_sync();
       cd* Z = fft_any(a, b, G.fq, true, lane, 64, WaveSync());
-#pragma unroll 1
-      for (int j = lane; j < G.W; j += 64) {
-        const cd z = Z[j];
-        cons(r, j, z.x);
-        if (two) cons(r + 1, j, z.y);
+      for (int j0 = 0; j0 < G.W; j0 += 64 * JCH) {
+        if (!PRE || j0 > 0) load_rows<JCH>(ld, r, two, j0, lane, G.W, v0, v1);
+#pragma unroll
+        for (int u = 0; u < JCH; ++u) {
+          const int j = j0 + lane + 64 * u;
+          if (j < G.W) {
+            const cd z = Z[j];
+            use(r, j, z.x, v0[u]);
+            if (two) use(r + 1, j, z.y, v1[u]);
+          }
+        }
       }
       wave_sync();
     }
   }
+}
+
+// row_inv: consumer form, `cons(r, j, value)` (loads, if any, inside).
+template <class Cons>
+__device__ __forceinline__ void row_inv(const Geo& G, const Part& D, const cd* spec, cd* lds,
+                                        Cons&& cons) {
+  row_inv2<false>(G, D, spec, lds, [](int, int) { return 0; },
+                  [&](int r, int j, double v, int) { cons(r, j, v); });
 }
 
 // row_inv_fwd: inverse rows of one convolution, then (same rows, same wave)
@@ -497,13 +572,37 @@ __device__ __forceinline__ void col_conv(const Geo& G, const Part& D, cd* spec, 
   if (w < G.nfw) {
     cd* a = lds + w * 2 * G.lpad;
     cd* b = a + G.lpad;
+    const bool one = G.P <= 64 * kPCH;  // column and TF loads in one batch
     for (int k = D.gw0 + w; k < G.Qh; k += D.gws) {
       cd* col = spec + (size_t)k * G.H;
-      for (int p = lane; p < G.P; p += 64) a[p] = (p < G.H) ? col[p] : cmk(0.0, 0.0);
+      const cd* t = tf + (size_t)k * G.P;
+      cd tv[kPCH];
+      for (int p0 = 0; p0 < G.P; p0 += 64 * kPCH) {
+        cd cv[kPCH];
+#pragma unroll
+        for (int u = 0; u < kPCH; ++u) {
+          const int p = p0 + lane + 64 * u;
+          cv[u] = cmk(0.0, 0.0);
+          if (p < G.H) cv[u] = col[p];
+          if (one && p < G.P) tv[u] = t[p];
+        }
+#pragma unroll
+        for (int u = 0; u < kPCH; ++u) {
+          const int p = p0 + lane + 64 * u;
+          if (p < G.P) a[p] = cv[u];
+        }
+      }
       wave_sync();
       cd* Z = fft_any(a, b, G.fp, false, lane, 64, WaveSync());
-      const cd* t = tf + (size_t)k * G.P;
-      for (int p = lane; p < G.P; p += 64) Z[p] = cmul(Z[p], t[p]);
+      if (one) {
+#pragma unroll
+        for (int u = 0; u < kPCH; ++u) {
+          const int p = lane + 64 * u;
+          if (p < G.P) Z[p] = cmul(Z[p], tv[u]);
+        }
+      } else {
+        for (int p = lane; p < G.P; p += 64) Z[p] = cmul(Z[p], t[p]);
+      }
       wave_sync();
       cd* Y = fft_any(Z, (Z == a) ? b : a, G.fp, true, lane, 64, WaveSync());
       for (int p = lane; p < G.H; p += 64) col[p] = Y[p];

@@ -16,6 +16,13 @@
 
 namespace bsgp {
 
+// The phase kernels are sized for 4 waves per SIMD (<= 128 VGPRs): four
+// 256-thread workgroups = four images per CU, so a 1024-image batch is
+// resident in one round on 256 CUs.
+#ifndef BSGP_OCC4
+#define BSGP_OCC4 __attribute__((amdgpu_waves_per_eu(4, 8)))
+#endif
+
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ double clipX(double x, double lo, double hi) {
   // X[X < lo] = lo; X[X > hi] = hi  (sgp.py:355-357)
@@ -621,13 +628,17 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
     ppass = po.evals;
   }
   double gd[1] = {0.0};
-  row_fwd(G, Pt, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) {
-    const int i = r * G.W + j;
-    const double g = B.ga[i];
-    const double d = D.d(B.xa[i], g);
-    gd[0] += d * g;
-    return d;
-  });
+  row_fwd2(
+      G, Pt, G.H, G.W, G.H, B.spec, lds,
+      [&](int r, int j) {
+        const int i = r * G.W + j;
+        return double2{B.xa[i], B.ga[i]};
+      },
+      [&](int, int, const double2& v) {
+        const double d = D.d(v.x, v.y);
+        gd[0] += d * v.y;
+        return d;
+      });
   team_sum<1>(gd, red, tm);
   team_end(st, tm);
   if (leader(tm)) {  // sgp.py:306-308 (memory shifts) + direction scalars
@@ -644,7 +655,7 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
 }
 
 // ----------------------------------------------------------- kernel: columns
-__global__ void __launch_bounds__(kBlock) k_col(SolveArgs A, int transpose) {
+__global__ void __launch_bounds__(kBlock) BSGP_OCC4 k_col(SolveArgs A, int transpose) {
   BSGP_LDS_VIEWS(A);
   const int img = team_img(A);
   const ImgState& st = A.st[img];
@@ -712,12 +723,26 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
 #pragma unroll
     for (int k = 0; k < N1; ++k) t1[k] = 0.0;
     double umax = 0.0;
-    row_inv(G, Pt, B.spec, lds, [&](int r, int j, double v) {
+    struct LsIn {
+      double x0, g, p0, bkv;
+    };
+    row_inv2<true, 4>(
+        G, Pt, B.spec, lds,
+        [&](int r, int j) {
+          const int i = r * G.W + j;
+          LsIn q;
+          q.x0 = B.xtf[i];
+          q.g = B.gns[i];
+          q.p0 = series ? B.pw[i] : 0.0;
+          q.bkv = bmap ? B.bks[i] : bks_scalar;
+          return q;
+        },
+        [&](int r, int j, double v, const LsIn& q) {
       const int i = r * G.W + j;
       B.dtf[i] = v;
-      const double g = B.gns[i];
-      const double x0 = B.xtf[i];
-      const double bkv = bmap ? B.bks[i] : bks_scalar;
+      const double g = q.g;
+      const double x0 = q.x0;
+      const double bkv = q.bkv;
       const double xt = x0 + lam * v;
       obj.template terms_m<MODE>(xt, xt + bkv, g, &t1[0]);
       if constexpr (adapt) {
@@ -727,7 +752,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
       if (series) {
         const double a = x0 + bkv;
         const double u = v / a;
-        const double p0 = B.pw[i];  // = fpow(a, beta-1), stored at the last accept
+        const double p0 = q.p0;  // = fpow(a, beta-1), stored at the last accept
         const double A0 = a * p0, B0 = g * p0;
         double um = 1.0;
 #pragma unroll
@@ -821,7 +846,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
     const double* dtf = B.dtf;
     const double* gns = B.gns;
     const double* bks = B.bks;
-    stream2<1>(
+    stream2<4>(
         Pt, npair,
         [&](int p) {
           struct V {
@@ -865,17 +890,31 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
   }
   // accept: x_tf += lam*d_tf; w = gn/den or gn*den^(b-2) (sgp.py:337-345, 790)
   const double lam_acc = lam;
-  row_fwd(G, Pt, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) {
-    const int i = r * G.W + j;
-    const double xt = B.xtf[i] + lam_acc * B.dtf[i];
-    B.xtf[i] = xt;
-    const double den = xt + (bmap ? B.bks[i] : bks_scalar);
-    const double g = B.gns[i];
-    if (P.variant != BSGP_VARIANT_BETA) return g / den;  // KL: w = gn/den
-    const double p = fpow(den, obj.beta - 1);
-    B.pw[i] = p;
-    return g * (p / den);
-  });
+  struct AcIn {
+    double x, d, g, bkv;
+  };
+  row_fwd2<4>(
+      G, Pt, G.H, G.W, G.H, B.spec, lds,
+      [&](int r, int j) {
+        const int i = r * G.W + j;
+        AcIn q;
+        q.x = B.xtf[i];
+        q.d = B.dtf[i];
+        q.g = B.gns[i];
+        q.bkv = bmap ? B.bks[i] : bks_scalar;
+        return q;
+      },
+      [&](int r, int j, const AcIn& q) {
+        const int i = r * G.W + j;
+        const double xt = q.x + lam_acc * q.d;
+        B.xtf[i] = xt;
+        const double den = xt + q.bkv;
+        const double g = q.g;
+        if (P.variant != BSGP_VARIANT_BETA) return g / den;  // KL: w = gn/den
+        const double p = fpow(den, obj.beta - 1);
+        B.pw[i] = p;
+        return g * (p / den);
+      });
   team_end(st, tm);
   if (leader(tm)) {
     if (A.out.flags)
@@ -895,7 +934,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
 // sgp.py:337-414 (= 785-879): g_new = g1(den) - AT(w), x += lam*d, the
 // Barzilai-Borwein step lengths with the tau alternation, the stop rules,
 // and the outputs once the image stops (sgp.py:424-438).
-__global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
+__global__ void __launch_bounds__(kBlock) BSGP_OCC4 k_bb(SolveArgs A) {
   BSGP_LDS_VIEWS(A);
   const int img = team_img(A);
   ImgState& st = A.st[img];
@@ -923,10 +962,23 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
   const double fv = st.fv, Dcoeff = st.Dcoeff, tol = st.tol, fold_last = st.Fold[P.M - 1];
   const double sc = st.sc;
   double bb[6] = {0, 0, 0, 0, 0, 0};  // bk, ck, sk2.sk2, yk2.yk2, sk.sk, x.x
-  row_inv(G, Pt, B.spec, lds, [&](int r, int j, double at) {
+  struct BbIn {
+    double p, x, g;
+  };
+  row_inv2<true, 2>(
+      G, Pt, B.spec, lds,
+      [&](int r, int j) {
+        const int i = r * G.W + j;
+        BbIn q;
+        q.p = beta_obj ? B.pw[i] : 1.0;
+        q.x = B.xa[i];
+        q.g = B.ga[i];
+        return q;
+      },
+      [&](int r, int j, double at, const BbIn& q) {
     const int i = r * G.W + j;
-    const double gnew = (beta_obj ? B.pw[i] : 1.0) - at;  // sgp.py:342 / 790
-    const double x = B.xa[i], g = B.ga[i];
+    const double gnew = q.p - at;  // sgp.py:342 / 790
+    const double x = q.x, g = q.g;
     const double d = D.d(x, g);
     const double sk = lam * d;
     const double xn = x + lam * d;
