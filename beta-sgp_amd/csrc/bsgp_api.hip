@@ -162,6 +162,15 @@ extern "C" {
 
 int32_t bsgp_abi_version(void) { return 1; }
 
+// Diagnostics (not in include/bsgp.h): per-phase shader cycles of a build
+// with -DBSGP_PHASE_PROF; returns BSGP_ERR_UNSUPPORTED otherwise.
+int bsgp_phase_prof(uint64_t* out, int32_t n, int32_t reset) {
+  hipError_t e = phase_prof(reinterpret_cast<unsigned long long*>(out), n, reset);
+  if (e == hipErrorNotSupported) return fail(BSGP_ERR_UNSUPPORTED, "built without BSGP_PHASE_PROF");
+  if (e != hipSuccess) return fail(BSGP_ERR_HIP, hipGetErrorString(e));
+  return BSGP_OK;
+}
+
 const char* bsgp_last_error(void) { return g_err.c_str(); }
 
 int bsgp_device_synchronize(void) {
@@ -217,7 +226,8 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
     return fail(BSGP_ERR_UNSUPPORTED, "FFT length has too many factors");
   }
   int maxlen = g.P > g.Q ? g.P : g.Q;
-  g.lpad = maxlen + 1;
+  // one FFT buffer also stages a row pair's stored spectrum (2*Qh, row_inv2); odd spreads banks
+  g.lpad = (maxlen + 1 > 2 * g.Qh ? maxlen + 1 : 2 * g.Qh) | 1;
   // LDS: nfw waves x 2 buffers, + reduction scratch
   const size_t red_bytes = (size_t)kWaves * kMaxRed * sizeof(double) + kSharedBytes;
   int nfw = kWaves;

@@ -24,7 +24,7 @@ namespace bsgp {
 #endif
 constexpr int kBlock = BSGP_BLOCK;  // threads per workgroup (one image per workgroup)
 constexpr int kWaves = kBlock / 64;
-constexpr int kMaxRed = 32;  // doubles reduced at once
+constexpr int kMaxRed = 24;  // doubles reduced at once
 constexpr int kSharedBytes = 512;  // LDS after the wave partials: reduced totals + scalars
 
 // Geometry of one conv plan (P x Q FFT grid, H x W image).
@@ -406,7 +406,10 @@ __device__ __forceinline__ void load_rows(LD& ld, int r, bool two, int j0, int l
 // (a, b real rows of length ncols zero-padded to Q) and stores the two half
 // spectra into column-major spec with leading dimension ld (>= nrows).
 // The input pixel is mk(r, j, ld(r, j)) (fused producer).
-template <int JCH = kJCH, class LD, class MK>
+// PF: the first operand batch of the wave's next row pair is issued before
+// the FFT of the current one (its latency hides under the FFT; the batch
+// registers stay live across it).
+template <int JCH = kJCH, bool PF = false, class LD, class MK>
 __device__ __forceinline__ void row_fwd2(const Geo& G, const Part& D, int nrows, int ncols,
                                          int ldim, cd* spec, cd* lds, LD&& ld, MK&& mk) {
   using V = decltype(ld(0, 0));
@@ -415,11 +418,13 @@ __device__ __forceinline__ void row_fwd2(const Geo& G, const Part& D, int nrows,
   if (w < G.nfw) {
     cd* a = lds + w * 2 * G.lpad;
     cd* b = a + G.lpad;
-    for (int r = 2 * (D.gw0 + w); r < nrows; r += 2 * D.gws) {
+    int r = 2 * (D.gw0 + w);
+    V v0[JCH], v1[JCH];
+    if (PF && r < nrows) load_rows<JCH>(ld, r, (r + 1) < nrows, 0, lane, ncols, v0, v1);
+    for (; r < nrows; r += 2 * D.gws) {
       const bool two = (r + 1) < nrows;
       for (int j0 = 0; j0 < G.Q; j0 += 64 * JCH) {
-        V v0[JCH], v1[JCH];
-        load_rows<JCH>(ld, r, two, j0, lane, ncols, v0, v1);
+        if (!PF || j0 > 0) load_rows<JCH>(ld, r, two, j0, lane, ncols, v0, v1);
 #pragma unroll
         for (int u = 0; u < JCH; ++u) {
           const int j = j0 + lane + 64 * u;
@@ -433,6 +438,8 @@ __device__ __forceinline__ void row_fwd2(const Geo& G, const Part& D, int nrows,
           }
         }
       }
+      const int rn = r + 2 * D.gws;
+      if (PF && rn < nrows) load_rows<JCH>(ld, rn, (rn + 1) < nrows, 0, lane, ncols, v0, v1);
       wave_sync();
       cd* Z = fft_any(a, b, G.fq, false, lane, 64, WaveSync());
       for (int k = lane; k < G.Qh; k += 64) {
@@ -478,26 +485,62 @@ __device__ __forceinline__ void gather_pair(const Geo& G, const cd* spec, int ld
   }
 }
 
+// LDS-DMA staging of one row pair's stored spectrum: F[k] = spec[k][r] and
+// F[Qh + k] = spec[k][r + 1] for k < Qh (global_load_lds_dwordx4: the LDS
+// destination is the wave-uniform base + 16 B * lane).  Needs lpad >= 2*Qh.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+__device__ __forceinline__ void stage_pair(const Geo& G, const cd* spec, int ld, int r, bool two,
+                                           cd* F, int lane) {
+  for (int k0 = 0; k0 < G.Qh; k0 += 64) {
+    const int k = k0 + lane;
+    if (k < G.Qh) {
+      const cd* col = spec + (size_t)k * ld + r;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)col, (lds_void_t*)(F + k0), 16, 0, 0);
+      if (two)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(col + 1), (lds_void_t*)(F + G.Qh + k0), 16,
+                                         0, 0);
+    }
+  }
+}
+// Full-length spectrum of the staged pair into `a` (as gather_pair).
+__device__ __forceinline__ void unpack_pair(const Geo& G, const cd* F, bool two, cd* a, int lane) {
+  for (int k = lane; k < G.Qh; k += 64) {
+    const cd A = F[k];
+    const cd B = two ? F[G.Qh + k] : cmk(0.0, 0.0);
+    a[k] = cmk(A.x - B.y, A.y + B.x);
+    if (k > 0 && G.Q - k >= G.Qh) a[G.Q - k] = cmk(A.x + B.y, B.x - A.y);
+  }
+}
+
 // row_inv2: inverse row transforms; use(r, j, value, ld(r, j)) consumes each
 // output pixel (j < W) of rows [0, H).  The 1/(P*Q) scale is folded into the
-// TF.  PRE: the first operand batch is issued before the spectrum gather, so
-// its latency hides under the gather and the FFT (costs its registers across
-// the FFT).
+// TF.  Software pipeline per wave: while row pair r is consumed, the stored
+// spectrum of the wave's next row pair streams into the buffer the FFT of r
+// left free (LDS-DMA), so its latency overlaps the operand loads and the
+// consumer of r; the first pair is gathered through registers.
+// PRE: the first operand batch is issued before the FFT (costs its registers
+// across the FFT).
 template <bool PRE, int JCH = kJCH, class LD, class USE>
 __device__ __forceinline__ void row_inv2(const Geo& G, const Part& D, const cd* spec, cd* lds,
                                          LD&& ld, USE&& use) {
   using V = decltype(ld(0, 0));
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (w < G.nfw) {
-    cd* a = lds + w * 2 * G.lpad;
-    cd* b = a + G.lpad;
-    for (int r = 2 * (D.gw0 + w); r < G.H; r += 2 * D.gws) {
+    cd* in = lds + w * 2 * G.lpad;
+    cd* other = in + G.lpad;
+    int r = 2 * (D.gw0 + w);
+    if (r < G.H) gather_pair(G, spec, G.H, r, (r + 1) < G.H, in, lane);
+    for (; r < G.H; r += 2 * D.gws) {
       const bool two = (r + 1) < G.H;
       V v0[JCH], v1[JCH];
       if (PRE) load_rows<JCH>(ld, r, two, 0, lane, G.W, v0, v1);
-      gather_pair(G, spec, G.H, r, two, a, lane);
       wave_sync();
-      cd* Z = fft_any(a, b, G.fq, true, lane, 64, WaveSync());
+      cd* Z = fft_any(in, other, G.fq, true, lane, 64, WaveSync());
+      cd* F = (Z == in) ? other : in;
+      const int rn = r + 2 * D.gws;
+      const bool next = rn < G.H, two_n = (rn + 1) < G.H;
+      if (next) stage_pair(G, spec, G.H, rn, two_n, F, lane);
       for (int j0 = 0; j0 < G.W; j0 += 64 * JCH) {
         if (!PRE || j0 > 0) load_rows<JCH>(ld, r, two, j0, lane, G.W, v0, v1);
 #pragma unroll
@@ -510,8 +553,15 @@ __device__ __forceinline__ void row_inv2(const Geo& G, const Part& D, const cd* 
           }
         }
       }
-      wave_sync();
+      if (next) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // staged pair landed
+        wave_sync();                                       // and Z fully consumed
+        unpack_pair(G, F, two_n, Z, lane);
+        in = Z;
+        other = F;
+      }
     }
+    wave_sync();
   }
 }
 

@@ -65,5 +65,7 @@ hipError_t launch_beta_div_deriv(int64_t n, const double* y, const double* x, do
 hipError_t launch_grad_parts(int64_t n, const double* den, const double* gn, double beta,
                              double* pow1, double* w, hipStream_t s);
 hipError_t set_solver_lds_limit(size_t bytes);
+constexpr int kPhaseSlots = 16;
+hipError_t phase_prof(unsigned long long* out, int n, int reset);
 
 }  // namespace bsgp

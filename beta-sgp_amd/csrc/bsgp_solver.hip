@@ -23,6 +23,52 @@ namespace bsgp {
 #define BSGP_OCC4 __attribute__((amdgpu_waves_per_eu(4, 8)))
 #endif
 
+// Operand batching of the inverse row passes (tuning knobs, see row_inv2)
+#ifndef BSGP_LS1_PRE
+#define BSGP_LS1_PRE false
+#endif
+#ifndef BSGP_LS1_JCH
+#define BSGP_LS1_JCH 2
+#endif
+#ifndef BSGP_BB_PRE
+#define BSGP_BB_PRE true
+#endif
+#ifndef BSGP_BB_JCH
+#define BSGP_BB_JCH 2
+#endif
+
+// Phase profile (builds with -DBSGP_PHASE_PROF only): thread 0 of every
+// workgroup adds the shader cycles it spent in each phase to g_phase[slot]
+// (tools/phase_prof.py reads them through bsgp_phase_prof).
+#ifdef BSGP_PHASE_PROF
+__device__ unsigned long long g_phase[kPhaseSlots];
+#define PH_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PH_ADD(slot, t0)                                                                 \
+  do {                                                                                   \
+    if (threadIdx.x == 0) atomicAdd(&g_phase[slot], __builtin_amdgcn_s_memtime() - (t0)); \
+  } while (0)
+#else
+#define PH_T(v)
+#define PH_ADD(slot, t0)
+#endif
+hipError_t phase_prof(unsigned long long* out, int n, int reset) {
+#ifdef BSGP_PHASE_PROF
+  if (n > kPhaseSlots) n = kPhaseSlots;
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess && out) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), n * sizeof(unsigned long long));
+  if (e == hipSuccess && reset) {
+    unsigned long long z[kPhaseSlots] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z);
+  }
+  return e;
+#else
+  (void)out;
+  (void)n;
+  (void)reset;
+  return hipErrorNotSupported;
+#endif
+}
+
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ double clipX(double x, double lo, double hi) {
   // X[X < lo] = lo; X[X > hi] = hi  (sgp.py:355-357)
@@ -434,6 +480,7 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
                   double qU) -> double {
     constexpr int NL = decltype(nlc)::value;
     constexpr int NT = NL + 6;  // sums | SA, SB, n_sat, n_list, n_overflow | slope
+    PH_T(tp0);
     double t[NT];
 #pragma unroll
     for (int k = 0; k < NT; ++k) t[k] = 0.0;
@@ -498,10 +545,12 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
       nstr = t[NL + 3];
     }
     ++passes;
+    PH_ADD(NL == 3 ? 10 : 12, tp0);
     return t[NL + 5];
   };
   // sum over the split bracket's list
   auto leval = [&](double lam) {
+    PH_T(tl0);
     double t[1] = {0.0};
     int k = 0;
     for (; k + 4 <= cnt; k += 4) {
@@ -516,6 +565,7 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
     }
     for (; k < cnt; ++k) t[0] += D.pv(ly[(size_t)k * LS + gt], lX[(size_t)k * LS + gt], lam);
     team_sum<1>(t, red, tm);
+    PH_ADD(11, tl0);
     const double lin = SA + lam * SB;
     return (hs ? lin + nsat * satv : lin) + t[0];
   };
@@ -577,6 +627,7 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
   const int img = team_img(A);
   ImgState& st = A.st[img];
   if (st.stop) return;
+  PH_T(tk0);
   Team tm = make_team(A, img, st);
   const Geo& G = A.g;
   const Part Pt = make_part(tm, G.nfw, G.W);
@@ -627,8 +678,10 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
     evals = po.evals;
     ppass = po.evals;
   }
+  PH_ADD(0, tk0);
+  PH_T(tk1);
   double gd[1] = {0.0};
-  row_fwd2(
+  row_fwd2<kJCH, true>(
       G, Pt, G.H, G.W, G.H, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
@@ -640,6 +693,8 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
         return d;
       });
   team_sum<1>(gd, red, tm);
+  PH_ADD(1, tk1);
+  PH_ADD(2, tk0);
   team_end(st, tm);
   if (leader(tm)) {  // sgp.py:306-308 (memory shifts) + direction scalars
     for (int k = 0; k < P.M_alpha - 1; ++k) st.Valpha[k] = st.Valpha[k + 1];
@@ -660,10 +715,12 @@ __global__ void __launch_bounds__(kBlock) BSGP_OCC4 k_col(SolveArgs A, int trans
   const int img = team_img(A);
   const ImgState& st = A.st[img];
   if (st.stop) return;
+  PH_T(tc0);
   const Team tm = make_team(A, img, st);
   Bufs B = slot_bufs(A, img, 0);
   load_tw_lds(A.g);
   col_conv(A.g, make_part(tm, A.g.nfw, A.g.W), B.spec, transpose ? A.g.tfAT : A.g.tfA, lds);
+  PH_ADD(3, tc0);
 }
 
 // ------------------------------- kernel: line search + accept + rows of w
@@ -679,6 +736,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
   const int img = team_img(A);
   ImgState& st = A.st[img];
   if (st.stop) return;
+  PH_T(tk0);
   Team tm = make_team(A, img, st);
   const Geo& G = A.g;
   const Part Pt = make_part(tm, G.nfw, G.W);
@@ -726,7 +784,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
     struct LsIn {
       double x0, g, p0, bkv;
     };
-    row_inv2<true, 4>(
+    row_inv2<BSGP_LS1_PRE, BSGP_LS1_JCH>(
         G, Pt, B.spec, lds,
         [&](int r, int j) {
           const int i = r * G.W + j;
@@ -767,6 +825,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
     });
     team_sum<N1>(t1, red, tm);
     if (series) rho = team_max(umax, red, tm);
+    PH_ADD(4, tk0);
 #pragma unroll
     for (int m = 0; m <= MS; ++m) {
       Pm[m] = t1[4 + m];
@@ -798,6 +857,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
       cb1[m] = cb1[m - 1] * (obj.beta - 1 - (m - 1)) / m;
     }
   }
+  PH_T(tk1);
   while (!accepted) {
     if (series && lam * rho <= kSeriesRho) {
       // closed-form trial: no pass over the image
@@ -846,7 +906,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
     const double* dtf = B.dtf;
     const double* gns = B.gns;
     const double* bks = B.bks;
-    stream2<4>(
+    stream2<2>(
         Pt, npair,
         [&](int p) {
           struct V {
@@ -888,12 +948,14 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
       break;
     }
   }
+  PH_ADD(5, tk1);
+  PH_T(tk2);
   // accept: x_tf += lam*d_tf; w = gn/den or gn*den^(b-2) (sgp.py:337-345, 790)
   const double lam_acc = lam;
   struct AcIn {
     double x, d, g, bkv;
   };
-  row_fwd2<4>(
+  row_fwd2<2, true>(
       G, Pt, G.H, G.W, G.H, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
@@ -915,6 +977,8 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
         B.pw[i] = p;
         return g * (p / den);
       });
+  PH_ADD(6, tk2);
+  PH_ADD(7, tk0);
   team_end(st, tm);
   if (leader(tm)) {
     if (A.out.flags)
@@ -939,6 +1003,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_OCC4 k_bb(SolveArgs A) {
   const int img = team_img(A);
   ImgState& st = A.st[img];
   if (st.stop) return;
+  PH_T(tk0);
   Team tm = make_team(A, img, st);
   const Geo& G = A.g;
   const Part Pt = make_part(tm, G.nfw, G.W);
@@ -965,7 +1030,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_OCC4 k_bb(SolveArgs A) {
   struct BbIn {
     double p, x, g;
   };
-  row_inv2<true, 2>(
+  row_inv2<BSGP_BB_PRE, BSGP_BB_JCH>(
       G, Pt, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
@@ -997,6 +1062,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_OCC4 k_bb(SolveArgs A) {
     B.gb[i] = gnew;
   });
   team_sum<6>(bb, red, tm);
+  PH_ADD(8, tk0);
   // Barzilai-Borwein (sgp.py:366-386)
   double alpha1, alpha2;
   if (bb[0] <= 0) {

@@ -1,0 +1,56 @@
+"""Per-phase cycle breakdown of the solver kernels (diagnostics).
+
+Build a profiling variant of the library and run the bench workload with it:
+
+    hipcc ... -DBSGP_PHASE_PROF -o beta-sgp_amd/libbsgp_prof.so ...   (tools/build_prof.sh)
+    BSGP_LIB=$PWD/beta-sgp_amd/libbsgp_prof.so python tools/phase_prof.py [--streams S]
+
+Thread 0 of every workgroup adds the shader cycles (s_memtime) it spent in
+each phase; the table is the mean per workgroup-iteration (image-iteration
+for team size 1), i.e. the latency one image spends in the phase.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "beta-sgp_amd")):
+    sys.path.insert(0, p)
+
+SLOTS = {0: "k_dir projection", 1: "k_dir row pass", 2: "k_dir total", 3: "k_col total",
+         4: "k_ls pass 1 (rows of A(d))", 5: "k_ls search loop", 6: "k_ls accept rows",
+         7: "k_ls total", 8: "k_bb rows + BB sums", 10: "  proj first pass",
+         11: "  proj list evals", 12: "  proj miss passes"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--streams", type=int, default=1)
+    ap.add_argument("--maxit", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=1024)
+    args = ap.parse_args()
+    import torch  # noqa: F401  (one HIP runtime, loaded before the library)
+    import bench
+    import _bsgp
+    import sgp
+    bench.torch = torch
+    L = _bsgp.lib()
+    L.bsgp_phase_prof.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+    buf = (ctypes.c_uint64 * 16)()
+    cfg = bench.CONFIGS["c3"]
+    gn, psf = bench.synth_batch(args.batch, cfg["n"], cfg["k"], cfg["nstars"], 0)
+    bkg = torch.full((args.batch,), 100.0, dtype=torch.float64, device="cuda")
+    kw = bench.solve_kwargs(args.maxit, None, args.streams, None)
+    sgp.sgp_betaDiv_batch(gn, psf, bkg, device_out=True, **kw)
+    _bsgp.check(L.bsgp_phase_prof(buf, 16, 1))  # reset after warm-up
+    out = sgp.sgp_betaDiv_batch(gn, psf, bkg, device_out=True, **kw)
+    _bsgp.check(L.bsgp_phase_prof(buf, 16, 1))
+    n = float(out["iters"].sum().item())
+    for k, name in SLOTS.items():
+        print(f"{name:32s} {buf[k] / n:12.0f} cycles per image-iteration"
+              + (" (2 launches)" if k == 3 else ""))
+
+
+if __name__ == "__main__":
+    main()
