@@ -110,6 +110,75 @@ BSGP_HD void bfly5(cd* v, bool inv) {
   v[3] = csub(t2, u2);
 }
 
+// exp(-2*pi*i*m/R) (forward) or its conjugate, for the internal twiddles of
+// the composite butterflies (R = 6: m = 1, 2; R = 9: m = 1, 2, 4).
+template <int R>
+BSGP_HD cd unit_root(int m, bool inv) {
+  double c = 1.0, s = 0.0;
+  if (R == 6) {
+    c = m == 1 ? 0.5 : -0.5;
+    s = 0.86602540378443864676;
+  } else if (R == 9) {
+    if (m == 1) {
+      c = 0.76604444311897803520;
+      s = 0.64278760968653932632;
+    } else if (m == 2) {
+      c = 0.17364817766693034885;
+      s = 0.98480775301220805936;
+    } else {
+      c = -0.93969262078590838405;
+      s = 0.34202014332566873304;
+    }
+  }
+  return cmk(c, inv ? s : -s);
+}
+
+template <int R>
+BSGP_HD void bfly_r(cd* v, bool inv);
+
+// Composite butterfly R = R1*R2 in registers (Cooley-Tukey, n = R2*n1 + n2,
+// k = k1 + R1*k2): R2 DFTs of length R1, internal twiddles w_R^(n2*k1), R1
+// DFTs of length R2.  One Stockham stage of radix 6 or 9 replaces two stages
+// (2*3, 3*3), halving the LDS round trips of those factors.
+template <int R1, int R2>
+BSGP_HD void bfly_comp(cd* v, bool inv) {
+  constexpr int R = R1 * R2;
+  cd y[R];
+#pragma unroll
+  for (int n2 = 0; n2 < R2; ++n2) {
+    cd t[R1];
+#pragma unroll
+    for (int n1 = 0; n1 < R1; ++n1) t[n1] = v[R2 * n1 + n2];
+    bfly_r<R1>(t, inv);
+#pragma unroll
+    for (int k1 = 0; k1 < R1; ++k1) y[n2 * R1 + k1] = t[k1];
+  }
+#pragma unroll
+  for (int n2 = 1; n2 < R2; ++n2)
+#pragma unroll
+    for (int k1 = 1; k1 < R1; ++k1)
+      y[n2 * R1 + k1] = cmul(y[n2 * R1 + k1], unit_root<R>((n2 * k1) % R, inv));
+#pragma unroll
+  for (int k1 = 0; k1 < R1; ++k1) {
+    cd t[R2];
+#pragma unroll
+    for (int n2 = 0; n2 < R2; ++n2) t[n2] = y[n2 * R1 + k1];
+    bfly_r<R2>(t, inv);
+#pragma unroll
+    for (int k2 = 0; k2 < R2; ++k2) v[k1 + R1 * k2] = t[k2];
+  }
+}
+
+template <int R>
+BSGP_HD void bfly_r(cd* v, bool inv) {
+  if constexpr (R == 2) bfly2(v);
+  if constexpr (R == 3) bfly3(v, inv);
+  if constexpr (R == 4) bfly4(v, inv);
+  if constexpr (R == 5) bfly5(v, inv);
+  if constexpr (R == 6) bfly_comp<3, 2>(v, inv);
+  if constexpr (R == 9) bfly_comp<3, 3>(v, inv);
+}
+
 // One Stockham stage with a compile-time radix. `lane` in [0, nlanes).
 template <int R>
 BSGP_HD void stage_fixed(const cd* in, cd* out, int n, int Ns, const cd* tw, bool inv,
@@ -218,12 +287,23 @@ struct RadixList {
   int r[kMaxStages];
 };
 
+#ifndef BSGP_FFT_COMPOSITE
+#define BSGP_FFT_COMPOSITE 1
+#endif
+// Stage radices of a static transform: 4s, then a 2 paired with a 3 as one
+// radix-6 stage, 3s paired as radix-9 stages, the rest, then 5s
+// (270 = 6*9*5: three LDS passes instead of five).
 constexpr RadixList factor_radices(int n) {
   RadixList L{0, {}};
   int m = n;
   while (m % 4 == 0) { L.r[L.n++] = 4; m /= 4; }
-  while (m % 2 == 0) { L.r[L.n++] = 2; m /= 2; }
-  while (m % 3 == 0) { L.r[L.n++] = 3; m /= 3; }
+  int c2 = 0, c3 = 0;
+  while (m % 2 == 0) { ++c2; m /= 2; }
+  while (m % 3 == 0) { ++c3; m /= 3; }
+  while (BSGP_FFT_COMPOSITE && c2 > 0 && c3 > 0) { L.r[L.n++] = 6; --c2; --c3; }
+  while (BSGP_FFT_COMPOSITE && c3 >= 2) { L.r[L.n++] = 9; c3 -= 2; }
+  while (c2 > 0) { L.r[L.n++] = 2; --c2; }
+  while (c3 > 0) { L.r[L.n++] = 3; --c3; }
   while (m % 5 == 0) { L.r[L.n++] = 5; m /= 5; }
   return L;
 }
@@ -244,10 +324,7 @@ BSGP_HD void stage_static(const cd* in, cd* out, const cd* tw, bool inv, int lan
 #pragma unroll
         for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw_at(tw, r * jm * twstep, inv));
       }
-      if constexpr (R == 2) bfly2(v);
-      if constexpr (R == 3) bfly3(v, inv);
-      if constexpr (R == 4) bfly4(v, inv);
-      if constexpr (R == 5) bfly5(v, inv);
+      bfly_r<R>(v, inv);
       const int od = (j / Ns) * Ns * R + jm;
 #pragma unroll
       for (int r = 0; r < R; ++r) out[od + r * Ns] = v[r];
@@ -260,10 +337,7 @@ BSGP_HD void stage_static(const cd* in, cd* out, const cd* tw, bool inv, int lan
       for (int r = 0; r < R; ++r) v[r] = in[j + r * nb];
       if (Ns > 1)
         for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw_at(tw, r * jm * twstep, inv));
-      if constexpr (R == 2) bfly2(v);
-      if constexpr (R == 3) bfly3(v, inv);
-      if constexpr (R == 4) bfly4(v, inv);
-      if constexpr (R == 5) bfly5(v, inv);
+      bfly_r<R>(v, inv);
       const int od = (j / Ns) * Ns * R + jm;
       for (int r = 0; r < R; ++r) out[od + r * Ns] = v[r];
     }

@@ -31,7 +31,7 @@ namespace bsgp {
 #define BSGP_LS1_JCH 2
 #endif
 #ifndef BSGP_BB_PRE
-#define BSGP_BB_PRE true
+#define BSGP_BB_PRE false
 #endif
 #ifndef BSGP_BB_JCH
 #define BSGP_BB_JCH 2
@@ -710,7 +710,7 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
 }
 
 // ----------------------------------------------------------- kernel: columns
-__global__ void __launch_bounds__(kBlock) BSGP_OCC4 k_col(SolveArgs A, int transpose) {
+__global__ void __launch_bounds__(kBlock) k_col(SolveArgs A, int transpose) {
   BSGP_LDS_VIEWS(A);
   const int img = team_img(A);
   const ImgState& st = A.st[img];
@@ -998,7 +998,7 @@ __global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
 // sgp.py:337-414 (= 785-879): g_new = g1(den) - AT(w), x += lam*d, the
 // Barzilai-Borwein step lengths with the tau alternation, the stop rules,
 // and the outputs once the image stops (sgp.py:424-438).
-__global__ void __launch_bounds__(kBlock) BSGP_OCC4 k_bb(SolveArgs A) {
+__global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
   BSGP_LDS_VIEWS(A);
   const int img = team_img(A);
   ImgState& st = A.st[img];
