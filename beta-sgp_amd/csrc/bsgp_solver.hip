@@ -30,6 +30,21 @@ namespace bsgp {
 #ifndef BSGP_LS1_JCH
 #define BSGP_LS1_JCH 2
 #endif
+#ifndef BSGP_DIR_ATTR
+#define BSGP_DIR_ATTR
+#endif
+#ifndef BSGP_LS_ATTR
+#define BSGP_LS_ATTR
+#endif
+#ifndef BSGP_PROJ_U
+#define BSGP_PROJ_U 4
+#endif
+#ifndef BSGP_DIR_JCH
+#define BSGP_DIR_JCH 4
+#endif
+#ifndef BSGP_DIR_PF
+#define BSGP_DIR_PF true
+#endif
 #ifndef BSGP_BB_PRE
 #define BSGP_BB_PRE false
 #endif
@@ -516,7 +531,7 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
         }
       }
     };
-    stream2<4>(
+    stream2<BSGP_PROJ_U>(
         Pt, npair,
         [&](int p) {
           struct V {
@@ -622,7 +637,7 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
 // sgp.py:306-325: memory shifts, y = x - alpha*X*g, projectDF(flux, y*D, D)
 // with every x(lambda) evaluation one streaming pass over (x, g), d = y - x,
 // d.g, and the row transforms of d.
-__global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
+__global__ void __launch_bounds__(kBlock) BSGP_DIR_ATTR k_dir(SolveArgs A) {
   BSGP_LDS_VIEWS(A);
   const int img = team_img(A);
   ImgState& st = A.st[img];
@@ -681,7 +696,7 @@ __global__ void __launch_bounds__(kBlock) k_dir(SolveArgs A) {
   PH_ADD(0, tk0);
   PH_T(tk1);
   double gd[1] = {0.0};
-  row_fwd2<kJCH, true>(
+  row_fwd2<BSGP_DIR_JCH, BSGP_DIR_PF>(
       G, Pt, G.H, G.W, G.H, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
@@ -728,7 +743,7 @@ __global__ void __launch_bounds__(kBlock) k_col(SolveArgs A, int transpose) {
 // the first pass is fused into the inverse row transforms that produce d_tf.
 // Then x_tf += lam*d_tf and the row transforms of AT's input w.
 template <int K, int MODE, bool ADAPT>
-__global__ void __launch_bounds__(kBlock) k_ls(SolveArgs A) {
+__global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   // first pass (fused into the inverse rows of A(d)): one trial lambda = 1,
   // which is where most non-stagnating iterations accept; later passes
   // stream K trial lambdas each.
