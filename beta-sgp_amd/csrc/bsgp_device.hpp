@@ -337,11 +337,16 @@ __device__ __forceinline__ double team_min(double v, double* red, Team& t) {
   return team_ext<false>(v, red, t);
 }
 
-// x**a for the divergence terms: exp(a*fast_log(x)) (bsgp_math.hpp).  For the
+// x**a for the divergence terms: fast_exp(a*fast_log(x)) (bsgp_math.hpp).  For the
 // exponents of this path (|a| = |beta-1| <~ 1, scaled data so |log x| <~ 20)
 // the error is a few ulp at most, at ~1/2.6 the cost of the general pow();
 // x <= 0 follows pow for the cases the iteration can produce.
-__device__ __forceinline__ double fpow(double x, double a) { return exp(a * fast_log(x)); }
+#ifndef BSGP_FAST_EXP
+#define BSGP_FAST_EXP 0  // measured: ocml exp is faster at k_ls's occupancy (A/B -2 %)
+#endif
+__device__ __forceinline__ double fpow(double x, double a) {
+  return BSGP_FAST_EXP ? fast_exp(a * fast_log(x)) : exp(a * fast_log(x));
+}
 
 // numpy-like max/min of two scalars (np.max([a, b]): NaN propagates)
 __device__ __forceinline__ double np_max2(double a, double b) {
@@ -957,9 +962,9 @@ struct Objective {
 // d betaDiv / d beta for one pixel (sgp.py:495), y = den, x = gn
 __device__ __forceinline__ double beta_deriv_px(double y, double x, double b) {
   const double ly = fast_log(y), lx = fast_log(x);
-  const double yb1 = exp((b - 1) * ly);
-  const double yb = exp(b * ly);
-  const double xb = exp(b * lx);
+  const double yb1 = fast_exp((b - 1) * ly);
+  const double yb = fast_exp(b * ly);
+  const double xb = fast_exp(b * lx);
   double t = -x * yb1 * ly / (b - 1);
   t = t + x * yb1 / ((b - 1) * (b - 1));
   t = t + xb * lx / (b * (b - 1));

@@ -59,8 +59,36 @@ BSGP_HD double fast_log(double x) {
   return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
 }
 
+// exp(t): t = k*ln2 + r with |r| <= ln2/2 (Cody-Waite, fma, exact), exp(r) by
+// its degree-13 Taylor polynomial (truncation < 4e-18 relative), scaled by 2^k
+// (v_ldexp_f64).  ~20 VALU instructions instead of ocml's ~42; error < 1 ulp
+// (tests/cpp/math_test.cpp).  Arguments that over/underflow, and NaN, go to
+// the library exp.
+BSGP_HD double fast_exp(double t) {
+  if (!(t > -708.0 && t < 709.0)) return std::exp(t);
+  const double inv_ln2 = 1.44269504088896338700e+00;
+  const double ln2_hi = 6.93147180369123816490e-01;
+  const double ln2_lo = 1.90821492927058770002e-10;
+  const double kd = std::rint(t * inv_ln2);
+  const double r = std::fma(-kd, ln2_lo, std::fma(-kd, ln2_hi, t));
+  double p = 1.6059043836821614599e-10;  // 1/13!
+  p = std::fma(p, r, 2.0876756987868098979e-09);  // 1/12!
+  p = std::fma(p, r, 2.5052108385441718775e-08);  // 1/11!
+  p = std::fma(p, r, 2.7557319223985890653e-07);  // 1/10!
+  p = std::fma(p, r, 2.7557319223985890653e-06);  // 1/9!
+  p = std::fma(p, r, 2.4801587301587301587e-05);  // 1/8!
+  p = std::fma(p, r, 1.9841269841269841270e-04);  // 1/7!
+  p = std::fma(p, r, 1.3888888888888888889e-03);  // 1/6!
+  p = std::fma(p, r, 8.3333333333333333333e-03);  // 1/5!
+  p = std::fma(p, r, 4.1666666666666666667e-02);  // 1/4!
+  p = std::fma(p, r, 1.6666666666666666667e-01);  // 1/3!
+  p = std::fma(p, r, 0.5);
+  p = std::fma(p, r * r, r);  // r + r^2 * (1/2 + r/6 + ...)
+  return std::ldexp(1.0 + p, (int)kd);
+}
+
 // x**a for positive x via exp(a*log x); for |a*log x| small (the beta-1
 // exponents of this path) the result carries ~1 ulp.
-BSGP_HD double fast_pow(double x, double a) { return std::exp(a * fast_log(x)); }
+BSGP_HD double fast_pow(double x, double a) { return fast_exp(a * fast_log(x)); }
 
 }  // namespace bsgp

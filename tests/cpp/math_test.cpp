@@ -24,6 +24,25 @@ int main() {
   check(1.0); check(2.0); check(0.5); check(1e-300); check(1e300);
   printf("fast_log max error %.3f ulp at x=%.17g\n", worst, worst_x);
   bool ok = worst < 1.0 && std::isnan(bsgp::fast_log(-1.0)) && std::isinf(bsgp::fast_log(0.0));
+  // fast_exp over the whole finite range and densely near 0 (the beta-1
+  // exponents of the line search)
+  double wexp = 0, wexp_t = 0;
+  auto check_exp = [&](double t) {
+    long double ref = expl((long double)t);
+    double got = bsgp::fast_exp(t);
+    double r = (double)ref;
+    double ulp = std::fabs(std::nextafter(r, INFINITY) - r);
+    double e = std::fabs((long double)got - ref) / ulp;
+    if (e > wexp) { wexp = e; wexp_t = t; }
+  };
+  std::uniform_real_distribution<double> te(-707.9, 708.9), ts(-2.0, 2.0);
+  for (int i = 0; i < 2000000; ++i) check_exp(te(rng));
+  for (int i = 0; i < 2000000; ++i) check_exp(ts(rng));
+  for (int i = 0; i < 200000; ++i) check_exp((uu(rng) - 1.25) * 1e-8);
+  check_exp(0.0); check_exp(1.0); check_exp(-1.0); check_exp(0.34657359027997264);
+  printf("fast_exp max error %.3f ulp at t=%.17g\n", wexp, wexp_t);
+  ok = ok && wexp < 1.0 && std::isinf(bsgp::fast_exp(1000.0)) && bsgp::fast_exp(-1000.0) == 0.0 &&
+       std::isnan(bsgp::fast_exp(NAN));
   printf(ok ? "math: all ok\n" : "math: FAIL\n");
   return ok ? 0 : 1;
 }

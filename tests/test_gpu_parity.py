@@ -160,6 +160,32 @@ def test_solve_matches_reference_linear(name, sgpmod):
     np.testing.assert_allclose(discr, fx["discr"], rtol=1e-7)
 
 
+@pytest.mark.parametrize("proj_cache", [0, 1])
+@pytest.mark.parametrize("name", ["lin64_beta", "lin256_kl", "lin256_beta", "lin64_beta_bmap"])
+def test_projection_pixel_lists_match_reference(name, proj_cache, sgpmod):
+    """projectDF with and without the pixel lists: the same
+    multiplier sequence (evaluation count E_p identical), the reference's
+    iterates within the solve tolerance; with the lists most evaluations cost
+    no full pass over the image."""
+    fx = golden(f"ref_{name}.npz")
+    kw = ref_kwargs(fx)
+    if not np.isnan(fx["flux"]):
+        kw["flux"] = np.float64(fx["flux"])
+    gns = fx["gn"].astype(np.float64)[None]
+    bkg = fx["bkg"][None] if fx["bkg"].ndim else float(fx["bkg"])
+    fn = sgpmod.sgp_betaDiv_batch if str(fx["fn"]) == "sgp_betaDiv" else sgpmod.sgp_batch
+    out = fn(gns, fx["psf"], bkg, team=1, proj_cache=proj_cache, **kw)
+    it = int(out["iters"][0])
+    assert it == int(fx["iters"])
+    assert rel(out["x"][0], fx["x"]) < SOLVE_RTOL, rel(out["x"][0], fx["x"])
+    np.testing.assert_allclose(out["discr"][0, :it + 1], fx["discr"], rtol=1e-7)
+    c = out["counters"][0]
+    if proj_cache:
+        assert 0 < c[6] < c[0], c  # full passes < evaluations
+    else:
+        assert c[6] == c[0] and c[7] == 0, c
+
+
 # --------------------------------------------------------- batch properties
 @pytest.mark.parametrize("team", [1, 2])
 def test_batch_is_bitwise_equal_to_single_solves(sgpmod, team):
