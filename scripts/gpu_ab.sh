@@ -1,22 +1,25 @@
 #!/bin/bash
-# Interleaved A/B/... benchmark of library variants, REPS rounds, median per variant.
-# Usage: bash scripts/gpu_ab.sh TAG REPS name... [-- bench args]   (name "base" = libbsgp.so)
+# Interleaved A/B/... benchmark, REPS rounds, median per variant.
+# Usage: bash scripts/gpu_ab.sh TAG REPS spec... [-- common bench args]
+#   spec = LIB[,extra,bench,args]   LIB "base" = libbsgp.so, else libbsgp_LIB.so
 set -o pipefail
 TAG=$1; REPS=$2; shift 2
-NAMES=()
-while [ $# -gt 0 ] && [ "$1" != "--" ]; do NAMES+=("$1"); shift; done
+SPECS=()
+while [ $# -gt 0 ] && [ "$1" != "--" ]; do SPECS+=("$1"); shift; done
 [ "$1" == "--" ] && shift
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
 for ((i=0; i<REPS; i++)); do
-  for V in "${NAMES[@]}"; do
+  for k in "${!SPECS[@]}"; do
+    IFS=',' read -ra PARTS <<< "${SPECS[$k]}"
+    V=${PARTS[0]}; EXTRA=("${PARTS[@]:1}")
     L=$PWD/beta-sgp_amd/libbsgp_$V.so; [ "$V" == "base" ] && L=$PWD/beta-sgp_amd/libbsgp.so
-    BSGP_LIB=$L timeout -k 10 300 python bench.py --no-cpu --steps 3 "$@" > gpurun_out/${TAG}_${V}_$i.json 2> gpurun_out/${TAG}_${V}_$i.err || { echo "bench $V failed"; tail -3 gpurun_out/${TAG}_${V}_$i.err; exit 3; }
+    BSGP_LIB=$L timeout -k 10 300 python bench.py --no-cpu --steps 3 "${EXTRA[@]}" "$@" > gpurun_out/${TAG}_${k}_$i.json 2> gpurun_out/${TAG}_${k}_$i.err || { echo "bench ${SPECS[$k]} failed"; tail -3 gpurun_out/${TAG}_${k}_$i.err; exit 3; }
   done
 done
-python - "$TAG" "$REPS" "${NAMES[@]}" <<'PY'
+python - "$TAG" "$REPS" "${SPECS[@]}" <<'PY'
 import json, sys, statistics
-tag, reps, names = sys.argv[1], int(sys.argv[2]), sys.argv[3:]
-for v in names:
-    vals = [json.load(open(f"gpurun_out/{tag}_{v}_{i}.json"))["value"] for i in range(reps)]
-    print(f"{v:10s} median {statistics.median(vals):9.0f}  all {[round(x) for x in vals]}")
+tag, reps, specs = sys.argv[1], int(sys.argv[2]), sys.argv[3:]
+for k, v in enumerate(specs):
+    vals = [json.load(open(f"gpurun_out/{tag}_{k}_{i}.json"))["value"] for i in range(reps)]
+    print(f"{v:28s} median {statistics.median(vals):9.0f}  all {[round(x) for x in vals]}")
 PY
