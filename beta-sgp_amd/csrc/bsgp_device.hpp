@@ -414,7 +414,7 @@ __device__ __forceinline__ void load_rows(LD& ld, int r, bool two, int j0, int l
 // PF: the first operand batch of the wave's next row pair is issued before
 // the FFT of the current one (its latency hides under the FFT; the batch
 // registers stay live across it).
-template <int JCH = kJCH, bool PF = false, class LD, class MK>
+template <int JCH = kJCH, bool PF = false, bool COMP = BSGP_FFT_COMPOSITE, class LD, class MK>
 __device__ __forceinline__ void row_fwd2(const Geo& G, const Part& D, int nrows, int ncols,
                                          int ldim, cd* spec, cd* lds, LD&& ld, MK&& mk) {
   using V = decltype(ld(0, 0));
@@ -446,7 +446,7 @@ __device__ __forceinline__ void row_fwd2(const Geo& G, const Part& D, int nrows,
       const int rn = r + 2 * D.gws;
       if (PF && rn < nrows) load_rows<JCH>(ld, rn, (rn + 1) < nrows, 0, lane, ncols, v0, v1);
       wave_sync();
-      cd* Z = fft_any(a, b, G.fq, false, lane, 64, WaveSync());
+      cd* Z = fft_any<COMP>(a, b, G.fq, false, lane, 64, WaveSync());
       for (int k = lane; k < G.Qh; k += 64) {
         cd ak, bk;
         r2c_split(Z, G.Q, k, &ak, &bk);
@@ -526,7 +526,7 @@ __device__ __forceinline__ void unpack_pair(const Geo& G, const cd* F, bool two,
 // consumer of r; the first pair is gathered through registers.
 // PRE: the first operand batch is issued before the FFT (costs its registers
 // across the FFT).
-template <bool PRE, int JCH = kJCH, class LD, class USE>
+template <bool PRE, int JCH = kJCH, bool COMP = BSGP_FFT_COMPOSITE, class LD, class USE>
 __device__ __forceinline__ void row_inv2(const Geo& G, const Part& D, const cd* spec, cd* lds,
                                          LD&& ld, USE&& use) {
   using V = decltype(ld(0, 0));
@@ -541,7 +541,7 @@ __device__ __forceinline__ void row_inv2(const Geo& G, const Part& D, const cd* 
       V v0[JCH], v1[JCH];
       if (PRE) load_rows<JCH>(ld, r, two, 0, lane, G.W, v0, v1);
       wave_sync();
-      cd* Z = fft_any(in, other, G.fq, true, lane, 64, WaveSync());
+      cd* Z = fft_any<COMP>(in, other, G.fq, true, lane, 64, WaveSync());
       cd* F = (Z == in) ? other : in;
       const int rn = r + 2 * D.gws;
       const bool next = rn < G.H, two_n = (rn + 1) < G.H;

@@ -293,15 +293,15 @@ struct RadixList {
 // Stage radices of a static transform: 4s, then a 2 paired with a 3 as one
 // radix-6 stage, 3s paired as radix-9 stages, the rest, then 5s
 // (270 = 6*9*5: three LDS passes instead of five).
-constexpr RadixList factor_radices(int n) {
+constexpr RadixList factor_radices(int n, bool comp = BSGP_FFT_COMPOSITE) {
   RadixList L{0, {}};
   int m = n;
   while (m % 4 == 0) { L.r[L.n++] = 4; m /= 4; }
   int c2 = 0, c3 = 0;
   while (m % 2 == 0) { ++c2; m /= 2; }
   while (m % 3 == 0) { ++c3; m /= 3; }
-  while (BSGP_FFT_COMPOSITE && c2 > 0 && c3 > 0) { L.r[L.n++] = 6; --c2; --c3; }
-  while (BSGP_FFT_COMPOSITE && c3 >= 2) { L.r[L.n++] = 9; c3 -= 2; }
+  while (comp && c2 > 0 && c3 > 0) { L.r[L.n++] = 6; --c2; --c3; }
+  while (comp && c3 >= 2) { L.r[L.n++] = 9; c3 -= 2; }
   while (c2 > 0) { L.r[L.n++] = 2; --c2; }
   while (c3 > 0) { L.r[L.n++] = 3; --c3; }
   while (m % 5 == 0) { L.r[L.n++] = 5; m /= 5; }
@@ -344,25 +344,26 @@ BSGP_HD void stage_static(const cd* in, cd* out, const cd* tw, bool inv, int lan
   }
 }
 
-template <int N, int S, int Ns, class Sync>
+template <int N, int S, int Ns, bool COMP, class Sync>
 BSGP_HD cd* stages_static(cd* in, cd* out, const cd* tw, bool inv, int lane, int nlanes,
                           Sync sync) {
-  constexpr RadixList L = factor_radices(N);
+  constexpr RadixList L = factor_radices(N, COMP);
   if constexpr (S < L.n) {
     constexpr int R = L.r[S];
     stage_static<R, N, Ns>(in, out, tw, inv, lane, nlanes);
     sync();
-    return stages_static<N, S + 1, Ns * R>(out, in, tw, inv, lane, nlanes, sync);
+    return stages_static<N, S + 1, Ns * R, COMP>(out, in, tw, inv, lane, nlanes, sync);
   } else {
     return in;
   }
 }
 
-// Transform of compile-time length N (must be 2/3/5-smooth).
-template <int N, class Sync>
+// Transform of compile-time length N (must be 2/3/5-smooth).  COMP: composite
+// radix-6/9 stages (fewer LDS round trips, ~20 more VGPRs live in the stage).
+template <int N, bool COMP = BSGP_FFT_COMPOSITE, class Sync>
 BSGP_HD cd* fft_run_static(cd* a, cd* b, const cd* tw, bool inv, int lane, int nlanes, Sync sync) {
   static_assert(factor_radices(N).n > 0, "N must be 2/3/5-smooth");
-  return stages_static<N, 0, 1>(a, b, tw, inv, lane, nlanes, sync);
+  return stages_static<N, 0, 1, COMP>(a, b, tw, inv, lane, nlanes, sync);
 }
 
 // Runtime length with compile-time fast paths for the hot grid sizes.  On the
@@ -372,19 +373,19 @@ BSGP_HD cd* fft_run_static(cd* a, cd* b, const cd* tw, bool inv, int lane, int n
 #if defined(__HIP_DEVICE_COMPILE__)
 extern __shared__ __attribute__((aligned(16))) char bsgp_dyn_lds[];
 #endif
-template <class Sync>
+template <bool COMP = BSGP_FFT_COMPOSITE, class Sync>
 BSGP_HD cd* fft_any(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlanes, Sync sync) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if (p.lds_tw >= 0) {
     const cd* t = reinterpret_cast<const cd*>(bsgp_dyn_lds + p.lds_tw);
-    if (p.n == 256) return fft_run_static<256>(a, b, t, inv, lane, nlanes, sync);
-    return fft_run_static<270>(a, b, t, inv, lane, nlanes, sync);
+    if (p.n == 256) return fft_run_static<256, COMP>(a, b, t, inv, lane, nlanes, sync);
+    return fft_run_static<270, COMP>(a, b, t, inv, lane, nlanes, sync);
   }
   return fft_run(a, b, p, inv, lane, nlanes, sync);
 #else
   switch (p.n) {
-    case 256: return fft_run_static<256>(a, b, p.tw, inv, lane, nlanes, sync);
-    case 270: return fft_run_static<270>(a, b, p.tw, inv, lane, nlanes, sync);
+    case 256: return fft_run_static<256, COMP>(a, b, p.tw, inv, lane, nlanes, sync);
+    case 270: return fft_run_static<270, COMP>(a, b, p.tw, inv, lane, nlanes, sync);
     default: return fft_run(a, b, p, inv, lane, nlanes, sync);
   }
 #endif

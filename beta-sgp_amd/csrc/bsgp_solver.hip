@@ -45,6 +45,17 @@ namespace bsgp {
 #ifndef BSGP_DIR_PF
 #define BSGP_DIR_PF true
 #endif
+// composite radix-6/9 FFT stages per row pass (the column pass always uses them):
+// fewer LDS round trips vs ~20 more live VGPRs
+#ifndef BSGP_DIR_COMP
+#define BSGP_DIR_COMP true
+#endif
+#ifndef BSGP_LS_COMP
+#define BSGP_LS_COMP true
+#endif
+#ifndef BSGP_BB_COMP
+#define BSGP_BB_COMP false
+#endif
 #ifndef BSGP_BB_PRE
 #define BSGP_BB_PRE false
 #endif
@@ -696,7 +707,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_DIR_ATTR k_dir(SolveArgs A) {
   PH_ADD(0, tk0);
   PH_T(tk1);
   double gd[1] = {0.0};
-  row_fwd2<BSGP_DIR_JCH, BSGP_DIR_PF>(
+  row_fwd2<BSGP_DIR_JCH, BSGP_DIR_PF, BSGP_DIR_COMP>(
       G, Pt, G.H, G.W, G.H, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
@@ -799,7 +810,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
     struct LsIn {
       double x0, g, p0, bkv;
     };
-    row_inv2<BSGP_LS1_PRE, BSGP_LS1_JCH>(
+    row_inv2<BSGP_LS1_PRE, BSGP_LS1_JCH, BSGP_LS_COMP>(
         G, Pt, B.spec, lds,
         [&](int r, int j) {
           const int i = r * G.W + j;
@@ -970,7 +981,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   struct AcIn {
     double x, d, g, bkv;
   };
-  row_fwd2<2, true>(
+  row_fwd2<2, true, BSGP_LS_COMP>(
       G, Pt, G.H, G.W, G.H, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
@@ -1045,7 +1056,7 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
   struct BbIn {
     double p, x, g;
   };
-  row_inv2<BSGP_BB_PRE, BSGP_BB_JCH>(
+  row_inv2<BSGP_BB_PRE, BSGP_BB_JCH, BSGP_BB_COMP>(
       G, Pt, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
