@@ -132,6 +132,8 @@ static int choose_team(const bsgp_plan_s* p, int B, int req) {
   const int rows2 = (g.H + 1) / 2;
   int tgeo = rows2 / g.nfw;
   if (g.Qh / g.nfw < tgeo) tgeo = g.Qh / g.nfw;
+  // (cooperative plans would fit two workgroups per CU, but one per CU measured
+  // faster on C4: 1262 vs 1180 it/s)
   int cap = p->ncu / B;
   int T = cap < tgeo ? cap : tgeo;
   if (req > 1 && req < T) T = req;
@@ -234,16 +236,20 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   size_t budget = 160 * 1024 / 4 - 256;  // four workgroups per CU
   p->wg_per_cu = 4;
   auto need = [&](int n) { return (size_t)n * 2 * g.lpad * sizeof(cd) + red_bytes; };
-  while (nfw > 1 && need(nfw) > budget) nfw--;
-  if (need(nfw) > budget) {
+  g.coop = 0;
+  if (need(kWaves) > budget) {
+    // transforms too long for a wave each at four workgroups per CU: the
+    // whole workgroup runs one transform at a time (cooperative passes)
+    g.coop = 1;
+    nfw = 1;
     budget = 160 * 1024 - 256;
-    p->wg_per_cu = 1;
-    nfw = kWaves;
-    while (nfw > 1 && need(nfw) > budget) nfw--;
-    if (need(nfw) > budget) {
+    if (need(1) > budget) {
       delete p;
       return fail(BSGP_ERR_UNSUPPORTED, "FFT length too large for one workgroup's LDS");
     }
+    p->wg_per_cu = (int)(budget / need(1));
+    if (p->wg_per_cu > 4) p->wg_per_cu = 4;
+    budget = 160 * 1024 / p->wg_per_cu - 256;
   }
   g.nfw = nfw;
   p->lds_fft_bytes = (size_t)nfw * 2 * g.lpad * sizeof(cd);

@@ -32,7 +32,8 @@ struct Geo {
   int H, W;      // image
   int P, Q;      // FFT grid (circular: P=H, Q=W)
   int Qh;        // stored half spectrum width = Q/2 + 1
-  int nfw;       // waves doing FFT work (each owns 2 LDS buffers)
+  int nfw;       // waves doing FFT work (each owns 2 LDS buffers); 1 in coop mode
+  int coop;      // 1: the whole workgroup runs one transform at a time (long rows/columns)
   int lpad;      // complex elements per LDS buffer (odd: spreads banks)
   FftPlan fp;    // length P (columns)
   FftPlan fq;    // length Q (rows)
@@ -407,6 +408,196 @@ __device__ __forceinline__ void load_rows(LD& ld, int r, bool two, int j0, int l
   }
 }
 
+// ---------------------------------------------------- cooperative passes
+// Geo::coop: transforms too long for one wave's share of the LDS (the 2048-point
+// rows and columns of config C4) run on the whole workgroup, one row pair or
+// column at a time, 256 lanes per Stockham stage and a workgroup barrier per
+// stage.  The team partition sees the workgroup as a single FFT worker
+// (nfw = 1): member m owns row pairs / columns m, m + T, ...
+struct BlockSync {
+  __device__ __forceinline__ void operator()() const { __syncthreads(); }
+};
+constexpr int kCCH = 4;  // elements per thread per load batch
+
+template <class LD, class MK>
+__device__ __forceinline__ void coop_row_fwd(const Geo& G, const Part& D, int nrows, int ncols,
+                                             int ldim, cd* spec, cd* lds, LD& ld, MK& mk) {
+  using V = decltype(ld(0, 0));
+  const int t = threadIdx.x;
+  const bool pair_ok = (ldim & 1) == 0;
+  cd* a = lds;
+  cd* b = lds + G.lpad;
+  for (int r = 2 * D.gw0; r < nrows; r += 2 * D.gws) {
+    const bool two = (r + 1) < nrows;
+    for (int j0 = 0; j0 < G.Q; j0 += kBlock * kCCH) {
+      V v0[kCCH], v1[kCCH];
+#pragma unroll
+      for (int u = 0; u < kCCH; ++u) {
+        const int j = j0 + t + kBlock * u;
+        if (j < ncols) {
+          v0[u] = ld(r, j);
+          if (two) v1[u] = ld(r + 1, j);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kCCH; ++u) {
+        const int j = j0 + t + kBlock * u;
+        if (j < G.Q) {
+          double va = 0.0, vb = 0.0;
+          if (j < ncols) {
+            va = mk(r, j, v0[u]);
+            if (two) vb = mk(r + 1, j, v1[u]);
+          }
+          a[j] = cmk(va, vb);
+        }
+      }
+    }
+    __syncthreads();
+    cd* Z = fft_wide(a, b, G.fq, false, t, kBlock, BlockSync());
+    for (int k = t; k < G.Qh; k += kBlock) {
+      cd ak, bk;
+      r2c_split(Z, G.Q, k, &ak, &bk);
+      store_pair(spec + (size_t)k * ldim + r, two, pair_ok, ak, bk);
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void coop_gather(const Geo& G, const cd* spec, int r, bool two, cd* a) {
+  const int t = threadIdx.x;
+  for (int k0 = 0; k0 < G.Qh; k0 += kBlock * kCCH) {
+    cd A[kCCH], B[kCCH];
+#pragma unroll
+    for (int u = 0; u < kCCH; ++u) {
+      const int k = k0 + t + kBlock * u;
+      if (k < G.Qh) {
+        const cd* col = spec + (size_t)k * G.H + r;
+        A[u] = col[0];
+        B[u] = two ? col[1] : cmk(0.0, 0.0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kCCH; ++u) {
+      const int k = k0 + t + kBlock * u;
+      if (k < G.Qh) {
+        a[k] = cmk(A[u].x - B[u].y, A[u].y + B[u].x);
+        if (k > 0 && G.Q - k >= G.Qh) a[G.Q - k] = cmk(A[u].x + B[u].y, B[u].x - A[u].y);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <class LD, class USE>
+__device__ __forceinline__ void coop_row_inv(const Geo& G, const Part& D, const cd* spec, cd* lds,
+                                             LD& ld, USE& use) {
+  using V = decltype(ld(0, 0));
+  const int t = threadIdx.x;
+  cd* a = lds;
+  cd* b = lds + G.lpad;
+  for (int r = 2 * D.gw0; r < G.H; r += 2 * D.gws) {
+    const bool two = (r + 1) < G.H;
+    coop_gather(G, spec, r, two, a);
+    cd* Z = fft_wide(a, b, G.fq, true, t, kBlock, BlockSync());
+    for (int j0 = 0; j0 < G.W; j0 += kBlock * kCCH) {
+      V v0[kCCH], v1[kCCH];
+#pragma unroll
+      for (int u = 0; u < kCCH; ++u) {
+        const int j = j0 + t + kBlock * u;
+        if (j < G.W) {
+          v0[u] = ld(r, j);
+          if (two) v1[u] = ld(r + 1, j);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kCCH; ++u) {
+        const int j = j0 + t + kBlock * u;
+        if (j < G.W) {
+          const cd z = Z[j];
+          use(r, j, z.x, v0[u]);
+          if (two) use(r + 1, j, z.y, v1[u]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <class CP>
+__device__ __forceinline__ void coop_row_inv_fwd(const Geo& G, const Part& D, cd* spec, cd* lds,
+                                                 CP& cp) {
+  const int t = threadIdx.x;
+  const bool pair_ok = (G.H & 1) == 0;
+  cd* a = lds;
+  cd* b = lds + G.lpad;
+  for (int r = 2 * D.gw0; r < G.H; r += 2 * D.gws) {
+    const bool two = (r + 1) < G.H;
+    coop_gather(G, spec, r, two, a);
+    cd* Z = fft_wide(a, b, G.fq, true, t, kBlock, BlockSync());
+    cd* in2 = (Z == a) ? b : a;
+    for (int j = t; j < G.Q; j += kBlock) {
+      double va = 0.0, vb = 0.0;
+      if (j < G.W) {
+        const cd z = Z[j];
+        va = cp(r, j, z.x);
+        if (two) vb = cp(r + 1, j, z.y);
+      }
+      in2[j] = cmk(va, vb);
+    }
+    __syncthreads();
+    cd* Y = fft_wide(in2, Z, G.fq, false, t, kBlock, BlockSync());
+    for (int k = t; k < G.Qh; k += kBlock) {
+      cd ak, bk;
+      r2c_split(Y, G.Q, k, &ak, &bk);
+      store_pair(spec + (size_t)k * G.H + r, two, pair_ok, ak, bk);
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void coop_col_conv(const Geo& G, const Part& D, cd* spec, const cd* tf,
+                                              cd* lds) {
+  const int t = threadIdx.x;
+  cd* a = lds;
+  cd* b = lds + G.lpad;
+  for (int k = D.gw0; k < G.Qh; k += D.gws) {
+    cd* col = spec + (size_t)k * G.H;
+    const cd* tk = tf + (size_t)k * G.P;
+    for (int p0 = 0; p0 < G.P; p0 += kBlock * kCCH) {
+      cd cv[kCCH];
+#pragma unroll
+      for (int u = 0; u < kCCH; ++u) {
+        const int p = p0 + t + kBlock * u;
+        cv[u] = (p < G.H) ? col[p] : cmk(0.0, 0.0);
+      }
+#pragma unroll
+      for (int u = 0; u < kCCH; ++u) {
+        const int p = p0 + t + kBlock * u;
+        if (p < G.P) a[p] = cv[u];
+      }
+    }
+    __syncthreads();
+    cd* Z = fft_wide(a, b, G.fp, false, t, kBlock, BlockSync());
+    for (int p0 = 0; p0 < G.P; p0 += kBlock * kCCH) {
+      cd tv[kCCH];
+#pragma unroll
+      for (int u = 0; u < kCCH; ++u) {
+        const int p = p0 + t + kBlock * u;
+        if (p < G.P) tv[u] = tk[p];
+      }
+#pragma unroll
+      for (int u = 0; u < kCCH; ++u) {
+        const int p = p0 + t + kBlock * u;
+        if (p < G.P) Z[p] = cmul(Z[p], tv[u]);
+      }
+    }
+    __syncthreads();
+    cd* Y = fft_wide(Z, (Z == a) ? b : a, G.fp, true, t, kBlock, BlockSync());
+    for (int p = t; p < G.H; p += kBlock) col[p] = Y[p];
+    __syncthreads();
+  }
+}
+
 // row_fwd2: for every pair of image rows (r, r+1) one wave FFTs z = a + i b
 // (a, b real rows of length ncols zero-padded to Q) and stores the two half
 // spectra into column-major spec with leading dimension ld (>= nrows).
@@ -414,9 +605,14 @@ __device__ __forceinline__ void load_rows(LD& ld, int r, bool two, int j0, int l
 // PF: the first operand batch of the wave's next row pair is issued before
 // the FFT of the current one (its latency hides under the FFT; the batch
 // registers stay live across it).
-template <int JCH = kJCH, bool PF = false, bool COMP = BSGP_FFT_COMPOSITE, class LD, class MK>
+template <int JCH = kJCH, bool PF = false, bool COMP = BSGP_FFT_COMPOSITE, bool COOP = false,
+          class LD, class MK>
 __device__ __forceinline__ void row_fwd2(const Geo& G, const Part& D, int nrows, int ncols,
                                          int ldim, cd* spec, cd* lds, LD&& ld, MK&& mk) {
+  if constexpr (COOP) {
+    coop_row_fwd(G, D, nrows, ncols, ldim, spec, lds, ld, mk);
+    return;
+  }
   using V = decltype(ld(0, 0));
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool pair_ok = (ldim & 1) == 0;
@@ -458,10 +654,11 @@ __device__ __forceinline__ void row_fwd2(const Geo& G, const Part& D, int nrows,
 }
 
 // row_fwd: producer form, `prod(r, j)` returns the input pixel.
-template <class Prod>
+template <bool COOP = false, class Prod>
 __device__ __forceinline__ void row_fwd(const Geo& G, const Part& D, int nrows, int ncols, int ldim,
                                         cd* spec, cd* lds, Prod&& prod) {
-  row_fwd2(G, D, nrows, ncols, ldim, spec, lds, prod, [](int, int, double v) { return v; });
+  row_fwd2<kJCH, false, BSGP_FFT_COMPOSITE, COOP>(G, D, nrows, ncols, ldim, spec, lds, prod,
+                                                  [](int, int, double v) { return v; });
 }
 
 // Rebuild the full-length spectrum of row pair (r, r+1) into `a`: each
@@ -526,9 +723,14 @@ __device__ __forceinline__ void unpack_pair(const Geo& G, const cd* F, bool two,
 // consumer of r; the first pair is gathered through registers.
 // PRE: the first operand batch is issued before the FFT (costs its registers
 // across the FFT).
-template <bool PRE, int JCH = kJCH, bool COMP = BSGP_FFT_COMPOSITE, class LD, class USE>
+template <bool PRE, int JCH = kJCH, bool COMP = BSGP_FFT_COMPOSITE, bool COOP = false, class LD,
+          class USE>
 __device__ __forceinline__ void row_inv2(const Geo& G, const Part& D, const cd* spec, cd* lds,
                                          LD&& ld, USE&& use) {
+  if constexpr (COOP) {
+    coop_row_inv(G, D, spec, lds, ld, use);
+    return;
+  }
   using V = decltype(ld(0, 0));
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (w < G.nfw) {
@@ -571,20 +773,25 @@ __device__ __forceinline__ void row_inv2(const Geo& G, const Part& D, const cd* 
 }
 
 // row_inv: consumer form, `cons(r, j, value)` (loads, if any, inside).
-template <class Cons>
+template <bool COOP = false, class Cons>
 __device__ __forceinline__ void row_inv(const Geo& G, const Part& D, const cd* spec, cd* lds,
                                         Cons&& cons) {
-  row_inv2<false>(G, D, spec, lds, [](int, int) { return 0; },
-                  [&](int r, int j, double v, int) { cons(r, j, v); });
+  row_inv2<false, kJCH, BSGP_FFT_COMPOSITE, COOP>(
+      G, D, spec, lds, [](int, int) { return 0; },
+      [&](int r, int j, double v, int) { cons(r, j, v); });
 }
 
 // row_inv_fwd: inverse rows of one convolution, then (same rows, same wave)
 // forward rows of the next one: `cp(r, j, value)` consumes the output pixel
 // and returns the next convolution's input pixel.  The spectrum is updated in
 // place (only this wave touches rows r, r+1).
-template <class CP>
+template <bool COOP = false, class CP>
 __device__ __forceinline__ void row_inv_fwd(const Geo& G, const Part& D, cd* spec, cd* lds,
                                             CP&& cp) {
+  if constexpr (COOP) {
+    coop_row_inv_fwd(G, D, spec, lds, cp);
+    return;
+  }
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool pair_ok = (G.H & 1) == 0;
   if (w < G.nfw) {
@@ -621,8 +828,13 @@ __device__ __forceinline__ void row_inv_fwd(const Geo& G, const Part& D, cd* spe
 // (contiguous, H rows) into its LDS buffer, zero-fills rows H..P-1, runs the
 // forward P-point FFT, multiplies by tf[k][:], runs the inverse FFT and
 // writes rows [0, H) back.  No workgroup barrier inside the pass.
+template <bool COOP = false>
 __device__ __forceinline__ void col_conv(const Geo& G, const Part& D, cd* spec, const cd* tf,
                                          cd* lds) {
+  if constexpr (COOP) {
+    coop_col_conv(G, D, spec, tf, lds);
+    return;
+  }
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (w < G.nfw) {
     cd* a = lds + w * 2 * G.lpad;

@@ -118,6 +118,10 @@ BSGP_HD cd unit_root(int m, bool inv) {
   if (R == 6) {
     c = m == 1 ? 0.5 : -0.5;
     s = 0.86602540378443864676;
+  } else if (R == 8) {
+    const double h = 0.70710678118654752440;  // sqrt(2)/2
+    c = m == 1 ? h : (m == 2 ? 0.0 : -h);
+    s = m == 2 ? 1.0 : h;
   } else if (R == 9) {
     if (m == 1) {
       c = 0.76604444311897803520;
@@ -176,6 +180,7 @@ BSGP_HD void bfly_r(cd* v, bool inv) {
   if constexpr (R == 4) bfly4(v, inv);
   if constexpr (R == 5) bfly5(v, inv);
   if constexpr (R == 6) bfly_comp<3, 2>(v, inv);
+  if constexpr (R == 8) bfly_comp<4, 2>(v, inv);
   if constexpr (R == 9) bfly_comp<3, 3>(v, inv);
 }
 
@@ -293,9 +298,11 @@ struct RadixList {
 // Stage radices of a static transform: 4s, then a 2 paired with a 3 as one
 // radix-6 stage, 3s paired as radix-9 stages, the rest, then 5s
 // (270 = 6*9*5: three LDS passes instead of five).
-constexpr RadixList factor_radices(int n, bool comp = BSGP_FFT_COMPOSITE) {
+// r8: radix-8 stages first (workgroup-wide transforms: 256 lanes, 2048 = 8*8*8*4).
+constexpr RadixList factor_radices(int n, bool comp = BSGP_FFT_COMPOSITE, bool r8 = false) {
   RadixList L{0, {}};
   int m = n;
+  while (r8 && m % 8 == 0) { L.r[L.n++] = 8; m /= 8; }
   while (m % 4 == 0) { L.r[L.n++] = 4; m /= 4; }
   int c2 = 0, c3 = 0;
   while (m % 2 == 0) { ++c2; m /= 2; }
@@ -344,26 +351,35 @@ BSGP_HD void stage_static(const cd* in, cd* out, const cd* tw, bool inv, int lan
   }
 }
 
-template <int N, int S, int Ns, bool COMP, class Sync>
+template <int N, int S, int Ns, bool COMP, bool R8, class Sync>
 BSGP_HD cd* stages_static(cd* in, cd* out, const cd* tw, bool inv, int lane, int nlanes,
                           Sync sync) {
-  constexpr RadixList L = factor_radices(N, COMP);
+  constexpr RadixList L = factor_radices(N, COMP, R8);
   if constexpr (S < L.n) {
     constexpr int R = L.r[S];
     stage_static<R, N, Ns>(in, out, tw, inv, lane, nlanes);
     sync();
-    return stages_static<N, S + 1, Ns * R, COMP>(out, in, tw, inv, lane, nlanes, sync);
+    return stages_static<N, S + 1, Ns * R, COMP, R8>(out, in, tw, inv, lane, nlanes, sync);
   } else {
     return in;
   }
 }
 
 // Transform of compile-time length N (must be 2/3/5-smooth).  COMP: composite
-// radix-6/9 stages (fewer LDS round trips, ~20 more VGPRs live in the stage).
-template <int N, bool COMP = BSGP_FFT_COMPOSITE, class Sync>
+// radix-6/9 stages (fewer LDS round trips, ~20 more VGPRs live in the stage);
+// R8: radix-8 stages first (for 256-lane workgroup transforms).
+template <int N, bool COMP = BSGP_FFT_COMPOSITE, bool R8 = false, class Sync>
 BSGP_HD cd* fft_run_static(cd* a, cd* b, const cd* tw, bool inv, int lane, int nlanes, Sync sync) {
   static_assert(factor_radices(N).n > 0, "N must be 2/3/5-smooth");
-  return stages_static<N, 0, 1, COMP>(a, b, tw, inv, lane, nlanes, sync);
+  return stages_static<N, 0, 1, COMP, R8>(a, b, tw, inv, lane, nlanes, sync);
+}
+
+// Workgroup-wide transform (all kBlock-style lanes, `sync` = workgroup
+// barrier): compile-time radix-8 plan for 2048 (config C4), runtime plan otherwise.
+template <class Sync>
+BSGP_HD cd* fft_wide(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlanes, Sync sync) {
+  if (p.n == 2048) return fft_run_static<2048, true, true>(a, b, p.tw, inv, lane, nlanes, sync);
+  return fft_run(a, b, p, inv, lane, nlanes, sync);
 }
 
 // Runtime length with compile-time fast paths for the hot grid sizes.  On the

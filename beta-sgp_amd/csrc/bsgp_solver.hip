@@ -266,6 +266,7 @@ __device__ __forceinline__ bool leader(const Team& t) { return t.m == 0 && threa
 // ------------------------------------------------------------ kernel: setup
 // sgp.py:163-298 (= 617-742): scaling, null pixels, flux, x0, initial
 // projection, x_tf = A(x), f, g and the scaling-matrix bounds.
+template <bool COOP>
 __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   BSGP_LDS_VIEWS(A);
   const int img = team_img(A);
@@ -365,12 +366,12 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   const double beta0 = A.in.beta0 ? A.in.beta0[img] : P.betaParam;
   Objective obj = make_obj(A, beta0);
   double fsum[3] = {0.0, 0.0, 0.0};  // K, T0, T1
-  row_fwd(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.xa[r * G.W + j]; });
+  row_fwd<COOP>(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.xa[r * G.W + j]; });
   team_sync(tm);
-  col_conv(G, D, B.spec, G.tfA, lds);
+  col_conv<COOP>(G, D, B.spec, G.tfA, lds);
   team_sync(tm);
   const bool beta_obj = P.variant == BSGP_VARIANT_BETA;
-  row_inv_fwd(G, D, B.spec, lds, [&](int r, int j, double v) {
+  row_inv_fwd<COOP>(G, D, B.spec, lds, [&](int r, int j, double v) {
     const int i = r * G.W + j;
     B.xtf[i] = v;
     const double den = v + (bmap ? B.bks[i] : bks_scalar);
@@ -385,20 +386,20 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   team_sum<3>(fsum, red, tm);
   team_sync(tm);  // publishes xtf / spec / pw
   const double fv = obj.combine(fsum[0], fsum[1], fsum[2], flux, (double)N);
-  col_conv(G, D, B.spec, G.tfAT, lds);
+  col_conv<COOP>(G, D, B.spec, G.tfAT, lds);
   team_sync(tm);
-  row_inv(G, D, B.spec, lds, [&](int r, int j, double at) {
+  row_inv<COOP>(G, D, B.spec, lds, [&](int r, int j, double at) {
     const int i = r * G.W + j;
     B.ga[i] = (beta_obj ? B.pw[i] : 1.0) - at;  // sgp.py:263 / 499
   });
   team_sync(tm);  // every row of spec read before it is overwritten
   // scaling-matrix bounds from AT(gn) (sgp.py:268-273)
-  row_fwd(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.gns[r * G.W + j]; });
+  row_fwd<COOP>(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.gns[r * G.W + j]; });
   team_sync(tm);
-  col_conv(G, D, B.spec, G.tfAT, lds);
+  col_conv<COOP>(G, D, B.spec, G.tfAT, lds);
   team_sync(tm);
   double ymin = INFINITY, ymax = -INFINITY;
-  row_inv(G, D, B.spec, lds, [&](int r, int j, double at) {
+  row_inv<COOP>(G, D, B.spec, lds, [&](int r, int j, double at) {
     const int i = r * G.W + j;
     const double bkv = bmap ? B.bks[i] : bks_scalar;
     const double y = (flux / (flux + bkv)) * at;
@@ -648,6 +649,7 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
 // sgp.py:306-325: memory shifts, y = x - alpha*X*g, projectDF(flux, y*D, D)
 // with every x(lambda) evaluation one streaming pass over (x, g), d = y - x,
 // d.g, and the row transforms of d.
+template <bool COOP>
 __global__ void __launch_bounds__(kBlock) BSGP_DIR_ATTR k_dir(SolveArgs A) {
   BSGP_LDS_VIEWS(A);
   const int img = team_img(A);
@@ -707,7 +709,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_DIR_ATTR k_dir(SolveArgs A) {
   PH_ADD(0, tk0);
   PH_T(tk1);
   double gd[1] = {0.0};
-  row_fwd2<BSGP_DIR_JCH, BSGP_DIR_PF, BSGP_DIR_COMP>(
+  row_fwd2<BSGP_DIR_JCH, BSGP_DIR_PF, BSGP_DIR_COMP, COOP>(
       G, Pt, G.H, G.W, G.H, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
@@ -736,6 +738,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_DIR_ATTR k_dir(SolveArgs A) {
 }
 
 // ----------------------------------------------------------- kernel: columns
+template <bool COOP>
 __global__ void __launch_bounds__(kBlock) k_col(SolveArgs A, int transpose) {
   BSGP_LDS_VIEWS(A);
   const int img = team_img(A);
@@ -745,7 +748,7 @@ __global__ void __launch_bounds__(kBlock) k_col(SolveArgs A, int transpose) {
   const Team tm = make_team(A, img, st);
   Bufs B = slot_bufs(A, img, 0);
   load_tw_lds(A.g);
-  col_conv(A.g, make_part(tm, A.g.nfw, A.g.W), B.spec, transpose ? A.g.tfAT : A.g.tfA, lds);
+  col_conv<COOP>(A.g, make_part(tm, A.g.nfw, A.g.W), B.spec, transpose ? A.g.tfAT : A.g.tfA, lds);
   PH_ADD(3, tc0);
 }
 
@@ -753,7 +756,7 @@ __global__ void __launch_bounds__(kBlock) k_col(SolveArgs A, int transpose) {
 // sgp.py:326-349 / 774-801: K trial lambdas per pass over (x_tf, d_tf, gn);
 // the first pass is fused into the inverse row transforms that produce d_tf.
 // Then x_tf += lam*d_tf and the row transforms of AT's input w.
-template <int K, int MODE, bool ADAPT>
+template <int K, int MODE, bool ADAPT, bool COOP>
 __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   // first pass (fused into the inverse rows of A(d)): one trial lambda = 1,
   // which is where most non-stagnating iterations accept; later passes
@@ -810,7 +813,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
     struct LsIn {
       double x0, g, p0, bkv;
     };
-    row_inv2<BSGP_LS1_PRE, BSGP_LS1_JCH, BSGP_LS_COMP>(
+    row_inv2<BSGP_LS1_PRE, BSGP_LS1_JCH, BSGP_LS_COMP, COOP>(
         G, Pt, B.spec, lds,
         [&](int r, int j) {
           const int i = r * G.W + j;
@@ -981,7 +984,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   struct AcIn {
     double x, d, g, bkv;
   };
-  row_fwd2<2, true, BSGP_LS_COMP>(
+  row_fwd2<2, true, BSGP_LS_COMP, COOP>(
       G, Pt, G.H, G.W, G.H, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
@@ -1024,6 +1027,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
 // sgp.py:337-414 (= 785-879): g_new = g1(den) - AT(w), x += lam*d, the
 // Barzilai-Borwein step lengths with the tau alternation, the stop rules,
 // and the outputs once the image stops (sgp.py:424-438).
+template <bool COOP>
 __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
   BSGP_LDS_VIEWS(A);
   const int img = team_img(A);
@@ -1056,7 +1060,7 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
   struct BbIn {
     double p, x, g;
   };
-  row_inv2<BSGP_BB_PRE, BSGP_BB_JCH, BSGP_BB_COMP>(
+  row_inv2<BSGP_BB_PRE, BSGP_BB_JCH, BSGP_BB_COMP, COOP>(
       G, Pt, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
@@ -1202,6 +1206,7 @@ __global__ void __launch_bounds__(kBlock) build_tf_kernel(Geo G, const double* k
 }
 
 // ------------------------------------------------------ A / AT standalone
+template <bool COOP>
 __global__ void __launch_bounds__(kBlock) apply_op_kernel(Geo G, int B, int transpose,
                                                           const double* x, double* out,
                                                           cd* specws, size_t spec_stride) {
@@ -1214,10 +1219,10 @@ __global__ void __launch_bounds__(kBlock) apply_op_kernel(Geo G, int B, int tran
     const double* xi = x + (size_t)img * N;
     double* oi = out + (size_t)img * N;
     const Part D = solo_part(G.nfw);
-    row_fwd(G, D, G.H, G.W, G.H, spec, lds, [&](int r, int j) { return xi[r * G.W + j]; });
+    row_fwd<COOP>(G, D, G.H, G.W, G.H, spec, lds, [&](int r, int j) { return xi[r * G.W + j]; });
     __syncthreads();
-    col_conv(G, D, spec, transpose ? G.tfAT : G.tfA, lds);
-    row_inv(G, D, spec, lds, [&](int r, int j, double v) { oi[r * G.W + j] = v; });
+    col_conv<COOP>(G, D, spec, transpose ? G.tfAT : G.tfA, lds);
+    row_inv<COOP>(G, D, spec, lds, [&](int r, int j, double v) { oi[r * G.W + j] = v; });
     __syncthreads();
   }
 }
@@ -1276,41 +1281,59 @@ __global__ void grad_parts_kernel(int64_t n, const double* den, const double* gn
 }
 
 // ----------------------------------------------------------- launchers
+// Kernels come in two builds: per-wave transforms (COOP = false) and, for long
+// rows/columns (Geo::coop), workgroup-cooperative ones; separate instantiations
+// keep each build's register allocation its own.
+template <bool COOP>
+static void launch_setup_t(const SolveArgs& a, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL((k_setup<COOP>), dim3(a.nimg * a.T), dim3(kBlock), lds, s, a);
+}
 hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL(k_setup, dim3(a.nimg * a.T), dim3(kBlock), lds, s, a);
+  if (a.g.coop)
+    launch_setup_t<true>(a, lds, s);
+  else
+    launch_setup_t<false>(a, lds, s);
   return hipGetLastError();
 }
-hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
+template <bool COOP>
+static void launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
   const dim3 grid(a.nimg * a.T), block(kBlock);
-  hipLaunchKernelGGL(k_dir, grid, block, lds, s, a);
-  hipLaunchKernelGGL(k_col, grid, block, lds, s, a, 0);
+  hipLaunchKernelGGL((k_dir<COOP>), grid, block, lds, s, a);
+  hipLaunchKernelGGL((k_col<COOP>), grid, block, lds, s, a, 0);
   // line-search kernel specialised on trial width, objective mode, adaptivity
   const bsgp_params& P = a.prm;
   const bool adapt = P.adapt_beta && P.variant == BSGP_VARIANT_BETA;
   const int mode = P.variant == BSGP_VARIANT_KL ? 0
                    : (P.betaParam == 0.0 || P.betaParam == 1.0 || a.in.beta0) ? -1
                                                                                 : 3;
+  if (COOP && K > 2) K = 2;  // cooperative builds carry trial widths 1 and 2
   if (adapt) {
-    hipLaunchKernelGGL((k_ls<1, -1, true>), grid, block, lds, s, a);
+    hipLaunchKernelGGL((k_ls<1, -1, true, COOP>), grid, block, lds, s, a);
   } else if (mode == 0) {
     switch (K) {
-      case 1: hipLaunchKernelGGL((k_ls<1, 0, false>), grid, block, lds, s, a); break;
-      case 2: hipLaunchKernelGGL((k_ls<2, 0, false>), grid, block, lds, s, a); break;
-      case 4: hipLaunchKernelGGL((k_ls<4, 0, false>), grid, block, lds, s, a); break;
-      default: hipLaunchKernelGGL((k_ls<8, 0, false>), grid, block, lds, s, a); break;
+      case 1: hipLaunchKernelGGL((k_ls<1, 0, false, COOP>), grid, block, lds, s, a); break;
+      case 2: hipLaunchKernelGGL((k_ls<2, 0, false, COOP>), grid, block, lds, s, a); break;
+      case 4: hipLaunchKernelGGL((k_ls<4, 0, false, false>), grid, block, lds, s, a); break;
+      default: hipLaunchKernelGGL((k_ls<8, 0, false, false>), grid, block, lds, s, a); break;
     }
   } else if (mode == 3) {
     switch (K) {
-      case 1: hipLaunchKernelGGL((k_ls<1, 3, false>), grid, block, lds, s, a); break;
-      case 2: hipLaunchKernelGGL((k_ls<2, 3, false>), grid, block, lds, s, a); break;
-      case 4: hipLaunchKernelGGL((k_ls<4, 3, false>), grid, block, lds, s, a); break;
-      default: hipLaunchKernelGGL((k_ls<8, 3, false>), grid, block, lds, s, a); break;
+      case 1: hipLaunchKernelGGL((k_ls<1, 3, false, COOP>), grid, block, lds, s, a); break;
+      case 2: hipLaunchKernelGGL((k_ls<2, 3, false, COOP>), grid, block, lds, s, a); break;
+      case 4: hipLaunchKernelGGL((k_ls<4, 3, false, false>), grid, block, lds, s, a); break;
+      default: hipLaunchKernelGGL((k_ls<8, 3, false, false>), grid, block, lds, s, a); break;
     }
   } else {
-    hipLaunchKernelGGL((k_ls<2, -1, false>), grid, block, lds, s, a);
+    hipLaunchKernelGGL((k_ls<2, -1, false, COOP>), grid, block, lds, s, a);
   }
-  hipLaunchKernelGGL(k_col, grid, block, lds, s, a, 1);
-  hipLaunchKernelGGL(k_bb, grid, block, lds, s, a);
+  hipLaunchKernelGGL((k_col<COOP>), grid, block, lds, s, a, 1);
+  hipLaunchKernelGGL((k_bb<COOP>), grid, block, lds, s, a);
+}
+hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
+  if (a.g.coop)
+    launch_iteration_t<true>(a, K, lds, s);
+  else
+    launch_iteration_t<false>(a, K, lds, s);
   return hipGetLastError();
 }
 hipError_t launch_build_tf(const Geo& g, const double* kc, cd* spec, cd* tf, double scale,
@@ -1321,8 +1344,12 @@ hipError_t launch_build_tf(const Geo& g, const double* kc, cd* spec, cd* tf, dou
 }
 hipError_t launch_apply_op(const Geo& g, int B, int transpose, const double* x, double* out,
                            cd* specws, size_t spec_stride, int grid, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL(apply_op_kernel, dim3(grid), dim3(kBlock), lds, s, g, B, transpose, x, out,
-                     specws, spec_stride);
+  if (g.coop)
+    hipLaunchKernelGGL((apply_op_kernel<true>), dim3(grid), dim3(kBlock), lds, s, g, B, transpose,
+                       x, out, specws, spec_stride);
+  else
+    hipLaunchKernelGGL((apply_op_kernel<false>), dim3(grid), dim3(kBlock), lds, s, g, B, transpose,
+                       x, out, specws, spec_stride);
   return hipGetLastError();
 }
 hipError_t launch_project_df(int n, double b, const double* c, const double* dia, ProjClip clip,
@@ -1352,21 +1379,32 @@ hipError_t launch_grad_parts(int64_t n, const double* den, const double* gn, dou
   return hipGetLastError();
 }
 hipError_t set_solver_lds_limit(size_t bytes) {
-  const void* fns[] = {(const void*)k_setup,
-                       (const void*)k_dir,
-                       (const void*)k_col,
-                       (const void*)k_ls<1, -1, true>,
-                       (const void*)k_ls<1, 0, false>,
-                       (const void*)k_ls<2, 0, false>,
-                       (const void*)k_ls<4, 0, false>,
-                       (const void*)k_ls<8, 0, false>,
-                       (const void*)k_ls<1, 3, false>,
-                       (const void*)k_ls<2, 3, false>,
-                       (const void*)k_ls<4, 3, false>,
-                       (const void*)k_ls<8, 3, false>,
-                       (const void*)k_ls<2, -1, false>,
-                       (const void*)k_bb,
-                       (const void*)apply_op_kernel,
+  const void* fns[] = {(const void*)k_setup<false>,
+                       (const void*)k_dir<false>,
+                       (const void*)k_col<false>,
+                       (const void*)k_ls<1, -1, true, false>,
+                       (const void*)k_ls<1, 0, false, false>,
+                       (const void*)k_ls<2, 0, false, false>,
+                       (const void*)k_ls<4, 0, false, false>,
+                       (const void*)k_ls<8, 0, false, false>,
+                       (const void*)k_ls<1, 3, false, false>,
+                       (const void*)k_ls<2, 3, false, false>,
+                       (const void*)k_ls<4, 3, false, false>,
+                       (const void*)k_ls<8, 3, false, false>,
+                       (const void*)k_ls<2, -1, false, false>,
+                       (const void*)k_bb<false>,
+                       (const void*)apply_op_kernel<false>,
+                       (const void*)k_setup<true>,
+                       (const void*)k_dir<true>,
+                       (const void*)k_col<true>,
+                       (const void*)k_ls<1, -1, true, true>,
+                       (const void*)k_ls<1, 0, false, true>,
+                       (const void*)k_ls<2, 0, false, true>,
+                       (const void*)k_ls<1, 3, false, true>,
+                       (const void*)k_ls<2, 3, false, true>,
+                       (const void*)k_ls<2, -1, false, true>,
+                       (const void*)k_bb<true>,
+                       (const void*)apply_op_kernel<true>,
                        (const void*)build_tf_kernel};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);

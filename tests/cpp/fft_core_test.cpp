@@ -114,6 +114,32 @@ int main() {
       }
     }
   }
+  // workgroup-wide radix-8 plan for 2048 (cooperative passes, 256 lanes run
+  // serially here) vs the runtime plan
+  for (int inv = 0; inv < 2; ++inv) {
+    const int n = 2048;
+    FftPlan p;
+    p.n = n;
+    plan_radices(n, p.radix, &p.ns);
+    std::vector<cd> tw = twiddles(n);
+    p.tw = tw.data();
+    std::vector<cd> a(n), b(n), c(n), d(n);
+    for (int i = 0; i < n; ++i) c[i] = a[i] = cmk(rand() / (double)RAND_MAX, rand() / (double)RAND_MAX);
+    cd* r1 = fft_run(a.data(), b.data(), p, inv, 0, 1, [] {});
+    {
+      std::vector<cd> x(c), y(n);
+      cd* r2 = fft_wide(x.data(), y.data(), p, inv, 0, 1, [] {});
+      double maxdiff = 0, maxref = 0;
+      for (int k = 0; k < n; ++k) {
+        maxdiff = fmax(maxdiff, fabs(r1[k].x - r2[k].x) + fabs(r1[k].y - r2[k].y));
+        maxref = fmax(maxref, fabs(r1[k].x) + fabs(r1[k].y));
+      }
+      if (!(maxdiff / maxref < 1e-14)) {
+        printf("FAIL wide n=2048 inv=%d diff %g\n", inv, maxdiff / maxref);
+        bad++;
+      }
+    }
+  }
   printf(bad ? "FFT core: %d failures\n" : "FFT core: all ok\n", bad);
   return bad ? 1 : 0;
 }

@@ -28,7 +28,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--streams", type=int, default=1)
     ap.add_argument("--maxit", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--config", default="c3")
     args = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime, loaded before the library)
     import bench
@@ -38,15 +39,16 @@ def main():
     L = _bsgp.lib()
     L.bsgp_phase_prof.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
     buf = (ctypes.c_uint64 * 16)()
-    cfg = bench.CONFIGS["c3"]
-    gn, psf = bench.synth_batch(args.batch, cfg["n"], cfg["k"], cfg["nstars"], 0)
-    bkg = torch.full((args.batch,), 100.0, dtype=torch.float64, device="cuda")
-    kw = bench.solve_kwargs(args.maxit, None, args.streams, None)
+    cfg = bench.CONFIGS[args.config]
+    B = args.batch or cfg["batch"]
+    gn, psf = bench.synth_batch(B, cfg["n"], cfg["k"], cfg["nstars"], 0, circular=cfg["circular"])
+    bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
+    kw = bench.solve_kwargs(args.maxit, None, args.streams, None, circular=cfg["circular"])
     sgp.sgp_betaDiv_batch(gn, psf, bkg, device_out=True, **kw)
     _bsgp.check(L.bsgp_phase_prof(buf, 16, 1))  # reset after warm-up
     out = sgp.sgp_betaDiv_batch(gn, psf, bkg, device_out=True, **kw)
     _bsgp.check(L.bsgp_phase_prof(buf, 16, 1))
-    n = float(out["iters"].sum().item())
+    n = float(out["iters"].sum().item()) * float(out["counters"][0, 5].item())  # x team size
     for k, name in SLOTS.items():
         print(f"{name:32s} {buf[k] / n:12.0f} cycles per image-iteration"
               + (" (2 launches)" if k == 3 else ""))
