@@ -96,10 +96,14 @@ def lib():
             L.bsgp_beta_div.argtypes = [i64, vp, vp, dbl, vp, vp]
             L.bsgp_beta_div_deriv.argtypes = [i64, vp, vp, dbl, vp, vp]
             L.bsgp_beta_div_grad_parts.argtypes = [i64, vp, vp, dbl, vp, vp, vp]
+            L.bsgp_extract_tiles.argtypes = [vp, i32, i32, vp, i32, i32, i32, vp, vp]
+            L.bsgp_coadd_tiles.argtypes = [vp, i32, i32, i32, vp, i32, i32, vp, vp, vp]
+            L.bsgp_fits_to_f64.argtypes = [vp, i64, i32, dbl, dbl, vp, vp]
             for name in ["bsgp_plan_create", "bsgp_plan_destroy", "bsgp_plan_info",
                          "bsgp_solve_device", "bsgp_solve_host", "bsgp_apply_operator",
                          "bsgp_project_df", "bsgp_beta_div", "bsgp_beta_div_deriv",
-                         "bsgp_beta_div_grad_parts", "bsgp_device_synchronize"]:
+                         "bsgp_beta_div_grad_parts", "bsgp_device_synchronize",
+                         "bsgp_extract_tiles", "bsgp_coadd_tiles", "bsgp_fits_to_f64"]:
                 getattr(L, name).restype = ctypes.c_int
             _lib = L
     return _lib
@@ -108,7 +112,8 @@ def lib():
 EXPORTED = ["bsgp_plan_create", "bsgp_plan_destroy", "bsgp_plan_info", "bsgp_solve_device",
             "bsgp_solve_host", "bsgp_apply_operator", "bsgp_project_df", "bsgp_beta_div",
             "bsgp_beta_div_deriv", "bsgp_beta_div_grad_parts", "bsgp_device_synchronize",
-            "bsgp_last_error", "bsgp_abi_version"]
+            "bsgp_last_error", "bsgp_abi_version", "bsgp_extract_tiles", "bsgp_coadd_tiles",
+            "bsgp_fits_to_f64"]
 
 
 def check(rc):

@@ -613,6 +613,34 @@ int bsgp_project_df(int64_t n, double b, const double* c, const double* dia, dou
   return BSGP_OK;
 }
 
+int bsgp_extract_tiles(const double* img, int32_t H, int32_t W, const int32_t* boxes, int32_t n,
+                       int32_t th, int32_t tw, double* out, void* stream) {
+  if (!img || !boxes || !out || H < 1 || W < 1 || n < 1 || th < 1 || tw < 1 || th > H || tw > W)
+    return fail(BSGP_ERR_ARG, "bad arguments");
+  if ((int64_t)n * th > 0x7fffffff) return fail(BSGP_ERR_ARG, "too many tile rows");
+  HIP_TRY(launch_extract_tiles(img, W, boxes, n, th, tw, out, (hipStream_t)stream));
+  return BSGP_OK;
+}
+
+int bsgp_coadd_tiles(const double* tiles, int32_t n, int32_t th, int32_t tw, const int32_t* boxes,
+                     int32_t H, int32_t W, double* mean, double* footprint, void* stream) {
+  if (!tiles || !boxes || !mean || H < 1 || W < 1 || n < 1 || n > 8192 || th < 1 || tw < 1)
+    return fail(BSGP_ERR_ARG, "bad arguments");
+  HIP_TRY(launch_coadd_tiles(tiles, n, th, tw, boxes, H, W, mean, footprint, (hipStream_t)stream));
+  return BSGP_OK;
+}
+
+int bsgp_fits_to_f64(const void* raw, int64_t n, int32_t bitpix, double bscale, double bzero,
+                     double* out, void* stream) {
+  if (!raw || !out || n < 0) return fail(BSGP_ERR_ARG, "bad arguments");
+  if (bitpix != 8 && bitpix != 16 && bitpix != 32 && bitpix != 64 && bitpix != -32 &&
+      bitpix != -64)
+    return fail(BSGP_ERR_ARG, "BITPIX must be 8, 16, 32, 64, -32 or -64");
+  if (n == 0) return BSGP_OK;
+  HIP_TRY(launch_fits_to_f64(raw, n, bitpix, bscale, bzero, out, (hipStream_t)stream));
+  return BSGP_OK;
+}
+
 int bsgp_beta_div(int64_t n, const double* y, const double* x, double beta, double* out,
                   void* stream) {
   if (n < 1 || n > 0x7fffffff || !y || !x || !out) return fail(BSGP_ERR_ARG, "bad arguments");

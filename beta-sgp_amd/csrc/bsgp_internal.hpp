@@ -65,6 +65,12 @@ hipError_t launch_beta_div_deriv(int64_t n, const double* y, const double* x, do
 hipError_t launch_grad_parts(int64_t n, const double* den, const double* gn, double beta,
                              double* pow1, double* w, hipStream_t s);
 hipError_t set_solver_lds_limit(size_t bytes);
+hipError_t launch_extract_tiles(const double* img, int W, const int* boxes, int n, int th, int tw,
+                                double* out, hipStream_t s);
+hipError_t launch_coadd_tiles(const double* tiles, int n, int th, int tw, const int* boxes, int H,
+                              int W, double* mean, double* footprint, hipStream_t s);
+hipError_t launch_fits_to_f64(const void* raw, int64_t n, int bitpix, double bscale, double bzero,
+                              double* out, hipStream_t s);
 constexpr int kPhaseSlots = 16;
 hipError_t phase_prof(unsigned long long* out, int n, int reset);
 

@@ -155,6 +155,31 @@ int bsgp_beta_div_deriv(int64_t n, const double* y, const double* x, double beta
 int bsgp_beta_div_grad_parts(int64_t n, const double* den, const double* gn, double beta,
                              double* pow1, double* w, void* stream);
 
+/* ---- data paths either side of the solver ---------- */
+
+/* Overlapping subdivision tiles of an [H][W] field: out[t] = img[y0:y1, x0:x1]
+ * for boxes[t] = {x0, y0, x1, y1} (device int32 [n][4], xyxy as
+ * restoration/utils.py:332-372 calculate_slice_bboxes returns them), every
+ * box exactly th x tw and inside the field.  Replaces create_subdivisions'
+ * Cutout2D cutouts (utils.py:375-386).  Asynchronous. */
+int bsgp_extract_tiles(const double* img, int32_t H, int32_t W, const int32_t* boxes, int32_t n,
+                       int32_t th, int32_t tw, double* out, void* stream);
+
+/* Mean co-add of n th x tw tiles at boxes into an [H][W] mosaic; footprint
+ * (may be NULL) = number of tiles covering each pixel; uncovered pixels are 0.
+ * Tiles are summed in index order (deterministic).  The same-WCS case of
+ * reproject_and_coadd (utils.py:389-395) with combine_function='mean' and no
+ * background matching.  n <= 8192.  Asynchronous. */
+int bsgp_coadd_tiles(const double* tiles, int32_t n, int32_t th, int32_t tw, const int32_t* boxes,
+                     int32_t H, int32_t W, double* mean, double* footprint, void* stream);
+
+/* FITS primary-array samples (big-endian, BITPIX 8/16/32/64/-32/-64) to f64:
+ * out[i] = BZERO + BSCALE * sample[i] (FITS standard 4.0 §5.3; IEEE samples
+ * exact).  raw: device copy of the data block, 8-byte aligned.  Replaces
+ * astropy.io.fits reads of results/*.fits and psf/*_img.fits.  Asynchronous. */
+int bsgp_fits_to_f64(const void* raw, int64_t n, int32_t bitpix, double bscale, double bzero,
+                     double* out, void* stream);
+
 int bsgp_device_synchronize(void);
 const char* bsgp_last_error(void);
 int32_t bsgp_abi_version(void);
