@@ -67,6 +67,15 @@ class Outputs(ctypes.Structure):
                 ("flags", _P), ("beta_final", _P), ("counters", _P)]
 
 
+class PsfModel(ctypes.Structure):
+    """bsgp_psf_model (include/bsgp.h)."""
+    _fields_ = [("hw", ctypes.c_int32), ("ngauss", ctypes.c_int32), ("ldeg", ctypes.c_int32),
+                ("sdeg", ctypes.c_int32), ("cos", ctypes.c_double), ("sin", ctypes.c_double),
+                ("ax", ctypes.c_double), ("ay", ctypes.c_double), ("sigma_inc", ctypes.c_double),
+                ("x_orig", ctypes.c_double), ("y_orig", ctypes.c_double), ("coeffs", _P),
+                ("ncoef", ctypes.c_int32)]
+
+
 _lib = None
 _lib_lock = threading.Lock()
 
@@ -99,11 +108,14 @@ def lib():
             L.bsgp_extract_tiles.argtypes = [vp, i32, i32, vp, i32, i32, i32, vp, vp]
             L.bsgp_coadd_tiles.argtypes = [vp, i32, i32, i32, vp, i32, i32, vp, vp, vp]
             L.bsgp_fits_to_f64.argtypes = [vp, i64, i32, dbl, dbl, vp, vp]
+            L.bsgp_psf_stamps.argtypes = [ctypes.POINTER(PsfModel), vp, i32, i32, i32, vp, vp]
+            L.bsgp_plan_set_psfs.argtypes = [vp, vp, i32, vp]
             for name in ["bsgp_plan_create", "bsgp_plan_destroy", "bsgp_plan_info",
                          "bsgp_solve_device", "bsgp_solve_host", "bsgp_apply_operator",
                          "bsgp_project_df", "bsgp_beta_div", "bsgp_beta_div_deriv",
                          "bsgp_beta_div_grad_parts", "bsgp_device_synchronize",
-                         "bsgp_extract_tiles", "bsgp_coadd_tiles", "bsgp_fits_to_f64"]:
+                         "bsgp_extract_tiles", "bsgp_coadd_tiles", "bsgp_fits_to_f64",
+                         "bsgp_psf_stamps", "bsgp_plan_set_psfs"]:
                 getattr(L, name).restype = ctypes.c_int
             _lib = L
     return _lib
@@ -113,7 +125,7 @@ EXPORTED = ["bsgp_plan_create", "bsgp_plan_destroy", "bsgp_plan_info", "bsgp_sol
             "bsgp_solve_host", "bsgp_apply_operator", "bsgp_project_df", "bsgp_beta_div",
             "bsgp_beta_div_deriv", "bsgp_beta_div_grad_parts", "bsgp_device_synchronize",
             "bsgp_last_error", "bsgp_abi_version", "bsgp_extract_tiles", "bsgp_coadd_tiles",
-            "bsgp_fits_to_f64"]
+            "bsgp_fits_to_f64", "bsgp_psf_stamps", "bsgp_plan_set_psfs"]
 
 
 def check(rc):
@@ -169,6 +181,16 @@ class Plan:
             self.h = None
 
     # -------------------------------------------------------------- operators
+    def set_psfs(self, psfs):
+        """Give image i of every later solve its own PSF psfs[i] ([n, kh, kw]
+        float64 CUDA tensor; bsgp_plan_set_psfs builds the n TF pairs on the device)."""
+        psfs = psfs.to(dtype=torch.float64).contiguous()
+        if psfs.dim() != 3 or tuple(psfs.shape[1:]) != (self.kh, self.kw):
+            raise ValueError(f"psfs must be [n, {self.kh}, {self.kw}]")
+        check(lib().bsgp_plan_set_psfs(self.h, _ptr(psfs), psfs.shape[0], current_stream()))
+        self.n_psf = psfs.shape[0]
+        return self
+
     def apply(self, x, transpose=False):
         """A(x) / AT(x) on a [B,H,W] (or [H,W]) float64 CUDA tensor."""
         x = x.contiguous()
@@ -235,6 +257,15 @@ def get_plan(H, W, psf, conv_mode):
             p = Plan(H, W, psf, conv_mode, dev)
             _plan_cache[key] = p
     return p
+
+
+def per_image_plan(H, W, psfs, conv_mode):
+    """A plan whose image i uses psfs[i] ([B, kh, kw], numpy or CUDA tensor);
+    not cached (it holds B transfer-function pairs)."""
+    require_gpu()
+    dev = psfs.to(dtype=torch.float64).contiguous() if torch.is_tensor(psfs) else to_dev(psfs)
+    p = Plan(H, W, dev[0].cpu().numpy(), conv_mode)
+    return p.set_psfs(dev)
 
 
 def to_dev(a):

@@ -5,6 +5,7 @@
 // of bsgp_solver.hip.  No PyTorch types cross this boundary.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -12,6 +13,7 @@
 #include <vector>
 
 #include "bsgp_internal.hpp"
+#include "bsgp_psf.hpp"
 
 using namespace bsgp;
 
@@ -50,7 +52,9 @@ struct bsgp_plan_s {
   int conv_mode = 0;
   Geo g{};
   cd* tw = nullptr;     // twiddles for P then Q
-  cd* tf = nullptr;     // tfA then tfAT, each Qh*P
+  cd* tf = nullptr;     // tfA then tfAT, each Qh*P (n_tf pairs after bsgp_plan_set_psfs)
+  int n_tf = 1;         // 1: one PSF for every image; else image i uses pair i (B == n_tf)
+  int kh = 0, kw = 0;   // PSF stamp shape of the plan
   size_t lds_fft_bytes = 0;
   size_t lds_bytes = 0;
   int wg_per_cu = 1;
@@ -204,6 +208,8 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   bsgp_plan p = new bsgp_plan_s();
   p->device = device;
   p->conv_mode = conv_mode;
+  p->kh = kh;
+  p->kw = kw;
   Geo& g = p->g;
   g.H = H;
   g.W = W;
@@ -386,6 +392,72 @@ int bsgp_plan_destroy(bsgp_plan p) {
   return BSGP_OK;
 }
 
+int bsgp_plan_set_psfs(bsgp_plan p, const double* psfs, int32_t n, void* stream) {
+  if (!p || !psfs || n < 1) return fail(BSGP_ERR_ARG, "bad arguments");
+  Geo& g = p->g;
+  const bool circ = p->conv_mode == BSGP_CONV_CIRCULAR;
+  // the device placement stores (no accumulation): the kernel must not wrap on the grid
+  if (!circ && (p->kh > g.P || p->kw > g.Q || p->kw > g.P || p->kh > g.Q))
+    return fail(BSGP_ERR_ARG, "per-image PSFs need a kernel no larger than the FFT grid");
+  HIP_TRY(hipSetDevice(p->device));
+  hipStream_t s = (hipStream_t)stream;
+  const size_t PQ = (size_t)g.P * g.Q, tfn = (size_t)g.Qh * g.P, specn = (size_t)g.P * g.Qh;
+  // chunks bound the placement/spectrum workspace (~256 MiB)
+  const size_t per = 2 * PQ * sizeof(double) + specn * sizeof(cd);
+  const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, (256u << 20) / per));
+  cd* tf = nullptr;
+  double* kc = nullptr;
+  cd* spec = nullptr;
+  double* sums = nullptr;
+  int rc = BSGP_OK;
+  if (hipMalloc(&tf, (size_t)n * 2 * tfn * sizeof(cd)) != hipSuccess ||
+      hipMalloc(&kc, (size_t)chunk * 2 * PQ * sizeof(double)) != hipSuccess ||
+      hipMalloc(&spec, (size_t)chunk * specn * sizeof(cd)) != hipSuccess ||
+      hipMalloc(&sums, (size_t)n * sizeof(double)) != hipSuccess)
+    rc = fail(BSGP_ERR_HIP, "per-image PSF allocation failed");
+  const double scale = 1.0 / ((double)g.P * (double)g.Q);
+  Geo gb = g;
+  gb.tf_stride = 0;
+  for (int c0 = 0; rc == BSGP_OK && c0 < n; c0 += chunk) {
+    const int m = std::min(chunk, n - c0);
+    cd* t = tf + (size_t)c0 * 2 * tfn;
+    if (hipMemsetAsync(kc, 0, (size_t)m * 2 * PQ * sizeof(double), s) != hipSuccess ||
+        launch_place_psfs(gb, m, psfs + (size_t)c0 * p->kh * p->kw, p->kh, p->kw, circ ? 1 : 0,
+                          kc, sums + c0, s) != hipSuccess ||
+        launch_build_tfs(gb, m, kc, 2 * PQ, spec, specn, t, 2 * tfn, scale, 0, p->lds_bytes,
+                         s) != hipSuccess ||
+        // circular: TF_AT = conj(TF_A) (sgp.py:110); linear: FFT of the transposed kernel
+        launch_build_tfs(gb, m, circ ? kc : kc + PQ, 2 * PQ, spec, specn, t + tfn, 2 * tfn,
+                         scale, circ ? 1 : 0, p->lds_bytes, s) != hipSuccess)
+      rc = fail(BSGP_ERR_HIP, "per-image TF launch failed");
+  }
+  std::vector<double> hs(n);
+  if (rc == BSGP_OK && (hipMemcpyAsync(hs.data(), sums, (size_t)n * sizeof(double),
+                                       hipMemcpyDeviceToHost, s) != hipSuccess ||
+                        hipStreamSynchronize(s) != hipSuccess))
+    rc = fail(BSGP_ERR_HIP, "per-image TF build failed");
+  for (int i = 0; rc == BSGP_OK && i < n; ++i)
+    if (!(std::fabs(hs[i] - 1.0) <= 1e4 * 2.220446049250313e-16)) {  // sgp.py:97-102
+      char b[160];
+      snprintf(b, sizeof b, "PSF %d is not normalized! sum(psf) - 1. = %.17g", i, hs[i] - 1.0);
+      rc = fail(BSGP_ERR_PSF, b);
+    }
+  if (kc) (void)hipFree(kc);
+  if (spec) (void)hipFree(spec);
+  if (sums) (void)hipFree(sums);
+  if (rc != BSGP_OK) {
+    if (tf) (void)hipFree(tf);
+    return rc;
+  }
+  if (p->tf) (void)hipFree(p->tf);
+  p->tf = tf;
+  p->n_tf = n;
+  g.tfA = tf;
+  g.tfAT = tf + tfn;
+  g.tf_stride = n > 1 ? 2 * tfn : 0;
+  return BSGP_OK;
+}
+
 int bsgp_plan_info(bsgp_plan p, int32_t* P, int32_t* Q, int64_t* slot_bytes,
                    int32_t* fft_waves) {
   if (!p) return fail(BSGP_ERR_ARG, "plan is NULL");
@@ -420,6 +492,8 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   if ((prm->init_recon == 1 || prm->scale_data == 2) && !in->x0)
     return fail(BSGP_ERR_ARG, "init_recon=1 and scale_data=2 need x0");
   if (!out || !out->x || !out->iters || !out->discr) return fail(BSGP_ERR_ARG, "outputs missing");
+  if (p->n_tf > 1 && B != p->n_tf)
+    return fail(BSGP_ERR_ARG, "the plan holds one PSF per image: B must equal its PSF count");
   HIP_TRY(hipSetDevice(p->device));
   rc = ensure_ws(p, (size_t)B);
   if (rc) return rc;
@@ -586,6 +660,8 @@ int bsgp_solve_host(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_i
 int bsgp_apply_operator(bsgp_plan p, int32_t B, int32_t transpose, const double* x, double* out,
                         void* stream) {
   if (!p || !x || !out || B < 1) return fail(BSGP_ERR_ARG, "bad arguments");
+  if (p->n_tf > 1 && B != p->n_tf)
+    return fail(BSGP_ERR_ARG, "the plan holds one PSF per image: B must equal its PSF count");
   HIP_TRY(hipSetDevice(p->device));
   const int grid = B < p->ncu * p->wg_per_cu ? B : p->ncu * p->wg_per_cu;
   const size_t stride = round_up((size_t)p->g.H * p->g.Qh, 16);
@@ -638,6 +714,38 @@ int bsgp_fits_to_f64(const void* raw, int64_t n, int32_t bitpix, double bscale, 
     return fail(BSGP_ERR_ARG, "BITPIX must be 8, 16, 32, 64, -32 or -64");
   if (n == 0) return BSGP_OK;
   HIP_TRY(launch_fits_to_f64(raw, n, bitpix, bscale, bzero, out, (hipStream_t)stream));
+  return BSGP_OK;
+}
+
+int bsgp_psf_stamps(const bsgp_psf_model* m, const double* xy, int32_t n, int32_t spatial,
+                    int32_t normalize, double* out, void* stream) {
+  if (!m || !out || n < 0 || (spatial && !xy) || !m->coeffs)
+    return fail(BSGP_ERR_ARG, "bad arguments");
+  if (m->hw < 0 || m->hw > 255 || m->ngauss < 1 || m->ldeg < 0 || m->sdeg < 0)
+    return fail(BSGP_ERR_ARG, "bad PSF model degrees or half width");
+  PsfModel M{};
+  M.ncomp = m->ngauss * (m->ldeg + 1) * (m->ldeg + 2) / 2;
+  const int nterm = (m->sdeg + 1) * (m->sdeg + 2) / 2;
+  const int need = spatial ? M.ncomp * nterm : M.ncomp;
+  if (M.ncomp > kPsfMaxLocal || need > kPsfMaxCoef)
+    return fail(BSGP_ERR_ARG, "PSF model has too many coefficients");
+  if (m->ncoef < need) return fail(BSGP_ERR_ARG, "too few PSF coefficients for the degrees");
+  if (n == 0) return BSGP_OK;
+  M.cosv = m->cos;
+  M.sinv = m->sin;
+  M.ax = m->ax;
+  M.ay = m->ay;
+  M.sig2 = m->sigma_inc * m->sigma_inc;
+  M.x_orig = m->x_orig;
+  M.y_orig = m->y_orig;
+  M.ngauss = m->ngauss;
+  M.ldeg = m->ldeg;
+  M.sdeg = m->sdeg;
+  M.hw = m->hw;
+  M.ncoef = need;
+  for (int i = 0; i < need; ++i) M.coef[i] = m->coeffs[i];
+  HIP_TRY(launch_psf_stamps(M, xy, n, spatial ? 1 : 0, normalize ? 1 : 0, out,
+                            (hipStream_t)stream));
   return BSGP_OK;
 }
 

@@ -39,7 +39,13 @@ struct Geo {
   FftPlan fq;    // length Q (rows)
   const cd* tfA;   // [Qh][P] transfer function of A, scaled by 1/(P*Q)
   const cd* tfAT;  // [Qh][P] transfer function of AT
+  size_t tf_stride;  // per-image PSFs: elements from image i's TF pair to i+1's (0: one PSF)
 };
+
+// Transfer function image `img` uses (bsgp_plan_set_psfs gives every image its own).
+__device__ __forceinline__ const cd* tf_of(const Geo& G, int img, int transpose) {
+  return (transpose ? G.tfAT : G.tfA) + (size_t)img * G.tf_stride;
+}
 
 // Copy the twiddle tables of the static-length transforms into their LDS slot
 // (plan.lds_tw); the caller's next workgroup barrier publishes them.

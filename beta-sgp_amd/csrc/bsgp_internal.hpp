@@ -53,6 +53,11 @@ hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s);
 hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s);
 hipError_t launch_build_tf(const Geo& g, const double* kc, cd* spec, cd* tf, double scale,
                            int conj, size_t lds, hipStream_t s);
+hipError_t launch_build_tfs(const Geo& g, int n, const double* kc, size_t kc_stride, cd* spec,
+                            size_t spec_stride, cd* tf, size_t tf_stride, double scale, int conj,
+                            size_t lds, hipStream_t s);
+hipError_t launch_place_psfs(const Geo& g, int n, const double* psfs, int kh, int kw, int circ,
+                             double* kc, double* sums, hipStream_t s);
 hipError_t launch_apply_op(const Geo& g, int B, int transpose, const double* x, double* out,
                            cd* specws, size_t spec_stride, int grid, size_t lds, hipStream_t s);
 hipError_t launch_project_df(int n, double b, const double* c, const double* dia, ProjClip clip,
@@ -71,6 +76,9 @@ hipError_t launch_coadd_tiles(const double* tiles, int n, int th, int tw, const 
                               int W, double* mean, double* footprint, hipStream_t s);
 hipError_t launch_fits_to_f64(const void* raw, int64_t n, int bitpix, double bscale, double bzero,
                               double* out, hipStream_t s);
+struct PsfModel;
+hipError_t launch_psf_stamps(const PsfModel& m, const double* xy, int n, int spatial,
+                             int normalize, double* out, hipStream_t s);
 constexpr int kPhaseSlots = 16;
 hipError_t phase_prof(unsigned long long* out, int n, int reset);
 

@@ -368,7 +368,7 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   double fsum[3] = {0.0, 0.0, 0.0};  // K, T0, T1
   row_fwd<COOP>(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.xa[r * G.W + j]; });
   team_sync(tm);
-  col_conv<COOP>(G, D, B.spec, G.tfA, lds);
+  col_conv<COOP>(G, D, B.spec, tf_of(G, img, 0), lds);
   team_sync(tm);
   const bool beta_obj = P.variant == BSGP_VARIANT_BETA;
   row_inv_fwd<COOP>(G, D, B.spec, lds, [&](int r, int j, double v) {
@@ -386,7 +386,7 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   team_sum<3>(fsum, red, tm);
   team_sync(tm);  // publishes xtf / spec / pw
   const double fv = obj.combine(fsum[0], fsum[1], fsum[2], flux, (double)N);
-  col_conv<COOP>(G, D, B.spec, G.tfAT, lds);
+  col_conv<COOP>(G, D, B.spec, tf_of(G, img, 1), lds);
   team_sync(tm);
   row_inv<COOP>(G, D, B.spec, lds, [&](int r, int j, double at) {
     const int i = r * G.W + j;
@@ -396,7 +396,7 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   // scaling-matrix bounds from AT(gn) (sgp.py:268-273)
   row_fwd<COOP>(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.gns[r * G.W + j]; });
   team_sync(tm);
-  col_conv<COOP>(G, D, B.spec, G.tfAT, lds);
+  col_conv<COOP>(G, D, B.spec, tf_of(G, img, 1), lds);
   team_sync(tm);
   double ymin = INFINITY, ymax = -INFINITY;
   row_inv<COOP>(G, D, B.spec, lds, [&](int r, int j, double at) {
@@ -748,7 +748,7 @@ __global__ void __launch_bounds__(kBlock) k_col(SolveArgs A, int transpose) {
   const Team tm = make_team(A, img, st);
   Bufs B = slot_bufs(A, img, 0);
   load_tw_lds(A.g);
-  col_conv<COOP>(A.g, make_part(tm, A.g.nfw, A.g.W), B.spec, transpose ? A.g.tfAT : A.g.tfA, lds);
+  col_conv<COOP>(A.g, make_part(tm, A.g.nfw, A.g.W), B.spec, tf_of(A.g, img, transpose), lds);
   PH_ADD(3, tc0);
 }
 
@@ -1178,11 +1178,17 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
 
 // --------------------------------------------------------- TF construction
 // tf[k][p] = FFT2(kc)[p][k] * scale (optionally conjugated); kc is P x Q real.
-__global__ void __launch_bounds__(kBlock) build_tf_kernel(Geo G, const double* kc, cd* spec,
-                                                          cd* tf, double scale, int conj) {
+// Workgroup b builds the TF of kc + b*kc_stride into tf + b*tf_stride.
+__global__ void __launch_bounds__(kBlock) build_tf_kernel(Geo G, const double* kc,
+                                                          size_t kc_stride, cd* spec,
+                                                          size_t spec_stride, cd* tf,
+                                                          size_t tf_stride, double scale, int conj) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cd* lds = reinterpret_cast<cd*>(smem);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  kc += blockIdx.x * kc_stride;
+  spec += blockIdx.x * spec_stride;
+  tf += blockIdx.x * tf_stride;
   load_tw_lds(G);
   // rows of the P x Q kernel grid -> column-major half spectrum (ld = P)
   row_fwd(G, solo_part(G.nfw), G.P, G.Q, G.P, spec, lds,
@@ -1205,6 +1211,43 @@ __global__ void __launch_bounds__(kBlock) build_tf_kernel(Geo G, const double* k
   }
 }
 
+// Per-image PSF stamps [n][kh][kw] -> circularly placed kernels for A and AT
+// on the P x Q grid (kc: [n][2][P*Q], zero-filled by the caller), the same
+// placement bsgp_plan_create makes on the host (bit-identical values: the
+// linear-mode sum is the same serial row-major loop).  sums[b] = sum(psf_b).
+__global__ void __launch_bounds__(kBlock) place_psfs_kernel(Geo G, const double* psfs, int kh,
+                                                            int kw, int circ, double* kc,
+                                                            double* sums) {
+  __shared__ double s_sum;
+  const double* psf = psfs + (size_t)blockIdx.x * kh * kw;
+  const size_t PQ = (size_t)G.P * G.Q;
+  double* kA = kc + (size_t)blockIdx.x * 2 * PQ;
+  double* kAT = kA + PQ;
+  if (threadIdx.x == 0) {
+    double s = 0;
+    for (int i = 0; i < kh * kw; ++i) s += psf[i];  // sgp.py:97-102 check / astropy normalisation
+    s_sum = s;
+    sums[blockIdx.x] = s;
+  }
+  __syncthreads();
+  const double s = s_sum;
+  for (int e = threadIdx.x; e < kh * kw; e += kBlock) {
+    const int u = e / kw, v = e % kw;
+    if (circ) {
+      // fftshift (sgp.py:109): kA[i][j] = psf[(i - H//2) mod H][(j - W//2) mod W]
+      const int i = (u + G.H / 2) % G.H, j = (v + G.W / 2) % G.W;
+      kA[(size_t)i * G.W + j] = psf[e];
+    } else {
+      // kernel/sum centred at k//2; AT: psf.T (sgp.py:157)
+      const double val = psf[e] / s;
+      const int a = ((u - kh / 2) % G.P + G.P) % G.P, b = ((v - kw / 2) % G.Q + G.Q) % G.Q;
+      kA[(size_t)a * G.Q + b] = val;
+      const int at = ((v - kw / 2) % G.P + G.P) % G.P, bt = ((u - kh / 2) % G.Q + G.Q) % G.Q;
+      kAT[(size_t)at * G.Q + bt] = val;
+    }
+  }
+}
+
 // ------------------------------------------------------ A / AT standalone
 template <bool COOP>
 __global__ void __launch_bounds__(kBlock) apply_op_kernel(Geo G, int B, int transpose,
@@ -1221,7 +1264,7 @@ __global__ void __launch_bounds__(kBlock) apply_op_kernel(Geo G, int B, int tran
     const Part D = solo_part(G.nfw);
     row_fwd<COOP>(G, D, G.H, G.W, G.H, spec, lds, [&](int r, int j) { return xi[r * G.W + j]; });
     __syncthreads();
-    col_conv<COOP>(G, D, spec, transpose ? G.tfAT : G.tfA, lds);
+    col_conv<COOP>(G, D, spec, tf_of(G, img, transpose), lds);
     row_inv<COOP>(G, D, spec, lds, [&](int r, int j, double v) { oi[r * G.W + j] = v; });
     __syncthreads();
   }
@@ -1338,8 +1381,19 @@ hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s
 }
 hipError_t launch_build_tf(const Geo& g, const double* kc, cd* spec, cd* tf, double scale,
                            int conj, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL(build_tf_kernel, dim3(1), dim3(kBlock), lds, s, g, kc, spec, tf, scale,
-                     conj);
+  return launch_build_tfs(g, 1, kc, 0, spec, 0, tf, 0, scale, conj, lds, s);
+}
+hipError_t launch_build_tfs(const Geo& g, int n, const double* kc, size_t kc_stride, cd* spec,
+                            size_t spec_stride, cd* tf, size_t tf_stride, double scale, int conj,
+                            size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL(build_tf_kernel, dim3(n), dim3(kBlock), lds, s, g, kc, kc_stride, spec,
+                     spec_stride, tf, tf_stride, scale, conj);
+  return hipGetLastError();
+}
+hipError_t launch_place_psfs(const Geo& g, int n, const double* psfs, int kh, int kw, int circ,
+                             double* kc, double* sums, hipStream_t s) {
+  hipLaunchKernelGGL(place_psfs_kernel, dim3(n), dim3(kBlock), 0, s, g, psfs, kh, kw, circ, kc,
+                     sums);
   return hipGetLastError();
 }
 hipError_t launch_apply_op(const Geo& g, int B, int transpose, const double* x, double* out,

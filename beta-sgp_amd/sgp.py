@@ -301,8 +301,10 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
                  use_original_SGP_Afunction=True, adapt_beta=False, betaParam=1.005, lr=1e-3,
                  lr_exp_param=0.1, schedule_lr=False, ls_spec=None, ls_series=None,
                  streams=None, team=None, proj_cache=None, device_out=False):
-    _check_psf(np.asarray(psf))
     torch = _B.torch
+    per_image = (psf.dim() if torch.is_tensor(psf) else np.ndim(psf)) == 3
+    if not per_image:
+        _check_psf(np.asarray(psf))
     _B.require_gpu()
     if not torch.is_tensor(gns):
         gns = _B.to_dev(np.asarray(gns, dtype=np.float64))
@@ -327,7 +329,12 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
         np.asarray(betaParams, dtype=np.float64), (Bn,)))
     fl = None if flux is None else _B.to_dev(np.broadcast_to(np.asarray(flux, dtype=np.float64),
                                                             (Bn,)))
-    plan = _B.get_plan(H, W, np.asarray(psf), mode)
+    if per_image:  # psf [B, kh, kw]: image i uses psf[i] (each checked as sgp.py:97-102)
+        if len(psf) != Bn:
+            raise ValueError("one PSF per image: psf must be [B, kh, kw]")
+        plan = _B.per_image_plan(H, W, psf, mode)
+    else:
+        plan = _B.get_plan(H, W, np.asarray(psf), mode)
     out = plan.solve(gns, bkgs, prm, flux=fl, x0=x0, beta0=b0)
     if device_out:
         return out
@@ -337,7 +344,8 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
 
 
 def sgp_batch(gns, psf, bkgs, **kw):
-    """KL-SGP on a batch [B, H, W] (one launch). Returns a dict of arrays:
+    """KL-SGP on a batch [B, H, W] (one launch); psf is one [kh, kw] PSF or
+    [B, kh, kw] (a PSF per image).  Returns a dict of arrays:
     x [B,H,W], iters [B], discr [B,MAXIT+1], times, crit, flags, counters."""
     return _solve_batch(_B.BSGP_VARIANT_KL, gns, psf, bkgs, **kw)
 

@@ -51,6 +51,12 @@ def subdivision_boxes(shape, subdiv_shape=(100, 100), overlap=10):
                       dtype=np.int32)
 
 
+def tile_centres(boxes):
+    """(x, y) pixel centre of every box: ((x0 + x1 - 1) / 2, (y0 + y1 - 1) / 2)."""
+    b = np.asarray(boxes, dtype=np.float64).reshape(-1, 4)
+    return np.stack([(b[:, 0] + b[:, 2] - 1) / 2, (b[:, 1] + b[:, 3] - 1) / 2], axis=1)
+
+
 def _field(image):
     torch = _B.torch
     if torch.is_tensor(image):
@@ -102,8 +108,12 @@ def sgp_subdivisions(image, psf, bkg, subdiv_shape=(256, 256), overlap=32, betaP
                      device_out=False, **sgp_kwargs):
     """Field -> overlapping subdivisions -> one batched beta-SGP solve -> mean
     mosaic.  ``bkg``: scalar, or a field-sized map (cut like the image, as the
-    application cuts its background map).  Returns (mosaic, footprint, solve
-    outputs); numpy unless device_out."""
+    application cuts its background map).  ``psf``: one stamp for every tile,
+    [n_tiles, kh, kw] stamps, or a DIAPL model (psf_calculate.PSF), which is
+    evaluated on the device at every tile centre (field pixel coordinates,
+    (x, y) = ((x0 + x1 - 1) / 2, (y0 + y1 - 1) / 2)) so each tile is solved
+    with its own PSF.  Returns (mosaic, footprint, solve outputs); numpy
+    unless device_out."""
     import sgp
     torch = _B.torch
     img = _field(image)
@@ -115,6 +125,8 @@ def sgp_subdivisions(image, psf, bkg, subdiv_shape=(256, 256), overlap=32, betaP
         bk = extract_tiles(b, boxes, subdiv_shape)
     else:
         bk = torch.full((len(boxes),), float(b), dtype=torch.float64, device="cuda")
+    if hasattr(psf, "stamps"):  # spatially varying DIAPL model: a stamp per tile centre
+        psf = psf.stamps(tile_centres(boxes), normalize=True, device_out=True)
     out = sgp.sgp_betaDiv_batch(tiles, psf, bk, betaParams=betaParams, device_out=True,
                                 **sgp_kwargs)
     mosaic, foot = coadd_tiles(out["x"], boxes, (H, W))

@@ -176,9 +176,43 @@ int bsgp_coadd_tiles(const double* tiles, int32_t n, int32_t th, int32_t tw, con
 /* FITS primary-array samples (big-endian, BITPIX 8/16/32/64/-32/-64) to f64:
  * out[i] = BZERO + BSCALE * sample[i] (FITS standard 4.0 §5.3; IEEE samples
  * exact).  raw: device copy of the data block, 8-byte aligned.  Replaces
- * astropy.io.fits reads of results/*.fits and psf/*_img.fits.  Asynchronous. */
+ * astropy.io.fits reads of the results/ and psf/ FITS files.  Asynchronous. */
 int bsgp_fits_to_f64(const void* raw, int64_t n, int32_t bitpix, double bscale, double bzero,
                      double* out, void* stream);
+
+/* DIAPL PSF model: the values of a psf*.bin.txt coefficient file
+ * (psf/psf_calculate.py:10-47 reads them in this order) plus the degrees the
+ * reference evaluates with (ldeg = 2, sdeg = 1: psf_calculate.py:24-25). */
+typedef struct {
+  int32_t hw;            /* stamp half width: stamps are (2hw+1) x (2hw+1)  (value 0) */
+  int32_t ngauss;        /* Gaussian components                           (value 3) */
+  int32_t ldeg;          /* local polynomial degree of calc_psf_pix (self.ldeg) */
+  int32_t sdeg;          /* spatial polynomial degree of init_psf (self.sdeg) */
+  double cos, sin;       /* values 5-6 */
+  double ax, ay;         /* values 7-8 */
+  double sigma_inc;      /* value 9 */
+  double x_orig, y_orig; /* values 12-13: origin of the spatial expansion */
+  const double* coeffs;  /* host: values 14.. (ngauss*(ldeg+1)(ldeg+2)/2 per spatial term) */
+  int32_t ncoef;
+} bsgp_psf_model;
+
+/* n PSF stamps [n][2hw+1][2hw+1] (device out).  spatial = 0: the local
+ * coefficients are coeffs[0:ncomp] for every stamp (get_psf_mat,
+ * psf_calculate.py:89-107; xy may be NULL); spatial = 1: the coefficients at
+ * field position xy[2i], xy[2i+1] (device, (x, y)) by the spatial expansion of
+ * init_psf (:140-165).  normalize = 1 divides each stamp by its numpy-order sum
+ * (normalize_psf_mat, :129-137).  Pixel (r, c) is calc_psf_pix(x = c - hw,
+ * y = r - hw) (:98-103).  Asynchronous. */
+int bsgp_psf_stamps(const bsgp_psf_model* model, const double* xy, int32_t n, int32_t spatial,
+                    int32_t normalize, double* out, void* stream);
+
+/* Per-image PSFs: replace the plan's transfer functions with n pairs built on
+ * the device from device PSF stamps [n][kh][kw] (the kh x kw the plan was
+ * created with; H x W in circular mode), each checked like sgp.py:97-102.
+ * Afterwards bsgp_solve_* and bsgp_apply_operator on this plan need B == n and
+ * image i is convolved with PSF i (the spatially varying PSF of each
+ * subdivision).  Synchronous. */
+int bsgp_plan_set_psfs(bsgp_plan plan, const double* psfs_dev, int32_t n, void* stream);
 
 int bsgp_device_synchronize(void);
 const char* bsgp_last_error(void);

@@ -150,3 +150,39 @@ def test_subdivision_chain_matches_oracle_per_tile():
     m_ref, c_ref = tiles_oracle.coadd_mean(ref, boxes, gn.shape)
     np.testing.assert_array_equal(foot, c_ref)
     assert np.linalg.norm(mosaic - m_ref) / np.linalg.norm(m_ref) < 1e-5
+
+
+@pytest.mark.gpu
+def test_subdivision_chain_with_spatial_psf_model():
+    """Each 128^2 subdivision solved with the DIAPL model's stamp at its centre
+    (bsgp_psf_stamps -> bsgp_plan_set_psfs), against the oracle solving every
+    tile with the oracle's stamp for that centre."""
+    import cpu_bench
+    import psf_calculate
+    import psf_oracle
+    import sgp_oracle
+    txt = os.path.join(GOLDEN, "psfccfbrd210048_1_1.bin.txt")
+    model = psf_calculate.PSF(txt)
+    rng = np.random.default_rng(6)
+    field = np.zeros((300, 300))
+    p = rng.integers(0, 300, (150, 2))
+    np.add.at(field, (p[:, 0], p[:, 1]), rng.pareto(1.5, 150) * 1000 + 100)
+    from scipy.signal import fftconvolve
+    gn = rng.poisson(np.clip(fftconvolve(field, cpu_bench.gaussian_psf(31), mode="same"), 0, None)
+                     + 100.0).astype(float)
+    kw = dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=5, alpha=10.0,
+              ccd_sat_level=65000.0, use_original_SGP_Afunction=False, schedule_lr=True,
+              adapt_beta=False, betaParam=1.05, verbose=False)
+    mosaic, foot, out = subdivisions.sgp_subdivisions(gn, model, 100.0, (128, 128), 40, **kw)
+    boxes = subdivisions.subdivision_boxes(gn.shape, (128, 128), 40)
+    hdr, coef = psf_oracle.read_model(txt)
+    stamps = psf_oracle.spatial_stamps(hdr, coef, subdivisions.tile_centres(boxes))
+    assert not np.allclose(stamps[0], stamps[-1])  # the PSF really varies over the field
+    tiles = tiles_oracle.extract_tiles(gn, boxes)
+    ref = np.stack([sgp_oracle.sgp_betaDiv(t, s, np.float64(100.0), **kw)[0]
+                    for t, s in zip(tiles, stamps)])
+    rel = np.linalg.norm(out["x"] - ref) / np.linalg.norm(ref)
+    assert rel < 1e-5, rel
+    m_ref, c_ref = tiles_oracle.coadd_mean(ref, boxes, gn.shape)
+    np.testing.assert_array_equal(foot, c_ref)
+    assert np.linalg.norm(mosaic - m_ref) / np.linalg.norm(m_ref) < 1e-5
