@@ -140,7 +140,11 @@ static int choose_team(const bsgp_plan_s* p, int B, int req) {
   // faster on C4: 1262 vs 1180 it/s)
   int cap = p->ncu / B;
   int T = cap < tgeo ? cap : tgeo;
-  if (req > 1 && req < T) T = req;
+  if (req > 1) {  // explicit request: up to what stays resident (members spin on each other)
+    const int res = p->ncu * p->wg_per_cu / B;
+    T = req < tgeo ? req : tgeo;
+    if (T > res) T = res;
+  }
   return T < 1 ? 1 : T;
 }
 

@@ -28,13 +28,16 @@ namespace bsgp {
 #define BSGP_LS1_PRE false
 #endif
 #ifndef BSGP_LS1_JCH
-#define BSGP_LS1_JCH 2
+#define BSGP_LS1_JCH 1
 #endif
 #ifndef BSGP_DIR_ATTR
 #define BSGP_DIR_ATTR
 #endif
+// k_ls at 3 waves/SIMD (<= 168 VGPRs; a few spills) with single-column operand
+// batches and plain radix stages in its row passes: +3 % end to end on C3
+// against 2 waves at 216 VGPRs (measured A/B).  Cooperative builds keep 1.
 #ifndef BSGP_LS_ATTR
-#define BSGP_LS_ATTR
+#define BSGP_LS_ATTR __attribute__((amdgpu_waves_per_eu(COOP ? 1 : (K <= 2 ? 3 : 2))))
 #endif
 #ifndef BSGP_PROJ_U
 #define BSGP_PROJ_U 4
@@ -51,7 +54,7 @@ namespace bsgp {
 #define BSGP_DIR_COMP true
 #endif
 #ifndef BSGP_LS_COMP
-#define BSGP_LS_COMP true
+#define BSGP_LS_COMP false
 #endif
 #ifndef BSGP_BB_COMP
 #define BSGP_BB_COMP false
