@@ -17,7 +17,7 @@ image vectors (8*N*(23 + 2*proj_passes + 3*ls_passes) per image-iteration plus
 16 B per projection-list entry read, all counted on the device; SURVEY §8d's
 per-evaluation formula is reported beside it) / the solve's duration measured
 with HIP events on the launch stream (the solve is the unit launched: setup +
-MAXIT x five phase kernels on two sub-batch streams); peak 8.0 TB/s.
+MAXIT x five phase kernels on three sub-batch streams); peak 8.0 TB/s.
 traffic: HBM bytes per solve from a rocprofv3 PMC run (profiles/), if present.
 cpu_baseline: the numpy oracle (oracle/sgp_oracle.py, a port of the reference)
 on a bounded sample of the same workload, process pool on this host's cores.

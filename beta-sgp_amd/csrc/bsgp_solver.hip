@@ -33,6 +33,9 @@ namespace bsgp {
 #ifndef BSGP_DIR_ATTR
 #define BSGP_DIR_ATTR
 #endif
+#ifndef BSGP_COL_ATTR
+#define BSGP_COL_ATTR
+#endif
 // k_ls at 3 waves/SIMD (<= 168 VGPRs; a few spills) with single-column operand
 // batches and plain radix stages in its row passes: +3 % end to end on C3
 // against 2 waves at 216 VGPRs (measured A/B).  Cooperative builds keep 1.
@@ -742,7 +745,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_DIR_ATTR k_dir(SolveArgs A) {
 
 // ----------------------------------------------------------- kernel: columns
 template <bool COOP>
-__global__ void __launch_bounds__(kBlock) k_col(SolveArgs A, int transpose) {
+__global__ void __launch_bounds__(kBlock) BSGP_COL_ATTR k_col(SolveArgs A, int transpose) {
   BSGP_LDS_VIEWS(A);
   const int img = team_img(A);
   const ImgState& st = A.st[img];

@@ -45,7 +45,7 @@ DEFAULT_COLUMNS = ['label', 'xcentroid', 'ycentroid', 'sky_centroid',
 
 LS_SPEC_DEFAULT = 2  # line-search trial lambdas evaluated per pass over the data
 LS_SERIES_DEFAULT = 1  # small line-search steps from the moment series (general beta)
-STREAMS_DEFAULT = 2  # sub-batch streams of a batched solve
+STREAMS_DEFAULT = 3  # sub-batch streams of a batched solve (+ the caller's = 4 HW queues; 4 sub-streams collapse under the default GPU_MAX_HW_QUEUES=4)
 TEAM_DEFAULT = 0  # workgroups per image: 0 = auto (spread small batches over the CUs)
 PROJ_CACHE_DEFAULT = 1  # projectDF evaluations inside a known root bracket read a pixel list
 
