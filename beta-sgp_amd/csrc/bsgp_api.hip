@@ -519,6 +519,14 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   a.vec_stride = p->vec_stride;
   a.lds_fft_bytes = p->lds_fft_bytes;
   a.T = T;
+  // k_col has no team reduction, so a team image may spread its columns over
+  // more workgroups than the team has (C4: 1025 columns, 256-member team)
+  a.Tc = T;
+  if (T > 1) {
+    const int nc = (p->g.Qh + p->g.nfw - 1) / p->g.nfw;
+    const int want = 4 * p->ncu / B;
+    a.Tc = std::max(T, std::min(nc, want));
+  }
   a.tpart = T > 1 ? p->tpart : nullptr;
   a.tctr = p->tctr;
   a.tfail = reinterpret_cast<int*>(p->tctr + B);
@@ -667,7 +675,11 @@ int bsgp_apply_operator(bsgp_plan p, int32_t B, int32_t transpose, const double*
   if (p->n_tf > 1 && B != p->n_tf)
     return fail(BSGP_ERR_ARG, "the plan holds one PSF per image: B must equal its PSF count");
   HIP_TRY(hipSetDevice(p->device));
-  const int grid = B < p->ncu * p->wg_per_cu ? B : p->ncu * p->wg_per_cu;
+  const int slots = p->ncu * p->wg_per_cu;
+  // few images: spread each over many workgroups (rows, columns, rows), one
+  // spectrum per image; many images: one persistent workgroup per image
+  const bool split = (size_t)B * 4 <= (size_t)slots;
+  const int grid = split ? B : (B < slots ? B : slots);
   const size_t stride = round_up((size_t)p->g.H * p->g.Qh, 16);
   if ((size_t)grid > p->opws_slots) {
     if (p->opws) HIP_TRY(hipFree(p->opws));
@@ -676,8 +688,12 @@ int bsgp_apply_operator(bsgp_plan p, int32_t B, int32_t transpose, const double*
     HIP_TRY(hipMalloc(&p->opws, (size_t)grid * stride * sizeof(cd)));
     p->opws_slots = grid;
   }
-  HIP_TRY(launch_apply_op(p->g, B, transpose, x, out, p->opws, stride, grid, p->lds_bytes,
-                          (hipStream_t)stream));
+  if (split)
+    HIP_TRY(launch_apply_op_split(p->g, B, transpose, x, out, p->opws, stride, slots / B,
+                                  p->lds_bytes, (hipStream_t)stream));
+  else
+    HIP_TRY(launch_apply_op(p->g, B, transpose, x, out, p->opws, stride, grid, p->lds_bytes,
+                            (hipStream_t)stream));
   return BSGP_OK;
 }
 

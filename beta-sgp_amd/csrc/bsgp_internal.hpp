@@ -39,6 +39,7 @@ struct SolveArgs {
   size_t lds_fft_bytes;
   // teams (T workgroups per image; T = 1: one workgroup, none of these used)
   int T;
+  int Tc;               // workgroups per image of k_col (no reductions there: not a team)
   double* tpart;        // [B][2][T][kMaxRed] reduction partials
   unsigned int* tctr;   // [B] barrier arrival counters, zeroed per solve
   int* tfail;           // set by a timed-out barrier spin
@@ -60,6 +61,9 @@ hipError_t launch_place_psfs(const Geo& g, int n, const double* psfs, int kh, in
                              double* kc, double* sums, hipStream_t s);
 hipError_t launch_apply_op(const Geo& g, int B, int transpose, const double* x, double* out,
                            cd* specws, size_t spec_stride, int grid, size_t lds, hipStream_t s);
+hipError_t launch_apply_op_split(const Geo& g, int B, int transpose, const double* x,
+                                 double* out, cd* specws, size_t spec_stride, int per, size_t lds,
+                                 hipStream_t s);
 hipError_t launch_project_df(int n, double b, const double* c, const double* dia, ProjClip clip,
                              double lam0, double dlam0, double tol_lam, int biter, int siter,
                              int max_projs, double* x, double* info, hipStream_t s);

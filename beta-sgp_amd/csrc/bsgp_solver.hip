@@ -747,11 +747,14 @@ __global__ void __launch_bounds__(kBlock) BSGP_DIR_ATTR k_dir(SolveArgs A) {
 template <bool COOP>
 __global__ void __launch_bounds__(kBlock) BSGP_COL_ATTR k_col(SolveArgs A, int transpose) {
   BSGP_LDS_VIEWS(A);
-  const int img = team_img(A);
+  // A.Tc workgroups per image (>= the team size T): columns only, no barrier
+  const int img = A.img0 + (A.Tc == 1 ? (int)blockIdx.x : (int)(blockIdx.x / (unsigned)A.Tc));
   const ImgState& st = A.st[img];
   if (st.stop) return;
   PH_T(tc0);
-  const Team tm = make_team(A, img, st);
+  Team tm{};
+  tm.T = A.Tc;
+  tm.m = A.Tc == 1 ? 0 : (int)(blockIdx.x % (unsigned)A.Tc);
   Bufs B = slot_bufs(A, img, 0);
   load_tw_lds(A.g);
   col_conv<COOP>(A.g, make_part(tm, A.g.nfw, A.g.W), B.spec, tf_of(A.g, img, transpose), lds);
@@ -1184,33 +1187,64 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
 
 // --------------------------------------------------------- TF construction
 // tf[k][p] = FFT2(kc)[p][k] * scale (optionally conjugated); kc is P x Q real.
-// Workgroup b builds the TF of kc + b*kc_stride into tf + b*tf_stride.
-__global__ void __launch_bounds__(kBlock) build_tf_kernel(Geo G, const double* kc,
-                                                          size_t kc_stride, cd* spec,
-                                                          size_t spec_stride, cd* tf,
-                                                          size_t tf_stride, double scale, int conj) {
+// Two launches over many workgroups (blockIdx.y = which kernel grid, for
+// per-image PSFs): rows of every grid into the column-major half spectrum
+// (ld = P), then the columns.  Cooperative plans transform each row/column
+// with the whole workgroup, like the solver's passes.
+template <bool COOP>
+__global__ void __launch_bounds__(kBlock) tf_rows_kernel(Geo G, const double* kc,
+                                                         size_t kc_stride, cd* spec,
+                                                         size_t spec_stride) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cd* lds = reinterpret_cast<cd*>(smem);
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  kc += blockIdx.x * kc_stride;
-  spec += blockIdx.x * spec_stride;
-  tf += blockIdx.x * tf_stride;
+  kc += blockIdx.y * kc_stride;
+  spec += blockIdx.y * spec_stride;
   load_tw_lds(G);
-  // rows of the P x Q kernel grid -> column-major half spectrum (ld = P)
-  row_fwd(G, solo_part(G.nfw), G.P, G.Q, G.P, spec, lds,
-          [&](int r, int j) { return kc[r * G.Q + j]; });
-  __syncthreads();
-  if (w < G.nfw) {
+  Part D = solo_part(G.nfw);
+  D.gw0 = blockIdx.x * G.nfw;
+  D.gws = gridDim.x * G.nfw;
+  row_fwd<COOP>(G, D, G.P, G.Q, G.P, spec, lds, [&](int r, int j) { return kc[r * G.Q + j]; });
+}
+
+template <bool COOP>
+__global__ void __launch_bounds__(kBlock) tf_cols_kernel(Geo G, const cd* spec,
+                                                         size_t spec_stride, cd* tf,
+                                                         size_t tf_stride, double scale,
+                                                         int conj) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cd* lds = reinterpret_cast<cd*>(smem);
+  spec += blockIdx.y * spec_stride;
+  tf += blockIdx.y * tf_stride;
+  load_tw_lds(G);
+  if constexpr (COOP) {
+    const int t = threadIdx.x;
+    cd* a = lds;
+    cd* b = lds + G.lpad;
+    for (int k = blockIdx.x; k < G.Qh; k += gridDim.x) {
+      const cd* col = spec + (size_t)k * G.P;
+      for (int p = t; p < G.P; p += kBlock) a[p] = col[p];
+      __syncthreads();
+      cd* Z = fft_wide(a, b, G.fp, false, t, kBlock, BlockSync());
+      cd* o = tf + (size_t)k * G.P;
+      for (int p = t; p < G.P; p += kBlock) {
+        const cd z = cscale(Z[p], scale);
+        o[p] = conj ? cconj(z) : z;
+      }
+      __syncthreads();
+    }
+  } else {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w >= G.nfw) return;
     cd* a = lds + w * 2 * G.lpad;
-    for (int k = w; k < G.Qh; k += G.nfw) {
+    for (int k = blockIdx.x * G.nfw + w; k < G.Qh; k += gridDim.x * G.nfw) {
       const cd* col = spec + (size_t)k * G.P;
       for (int p = lane; p < G.P; p += 64) a[p] = col[p];
       wave_sync();
       cd* Z = fft_any(a, a + G.lpad, G.fp, false, lane, 64, WaveSync());
-      cd* t = tf + (size_t)k * G.P;
+      cd* o = tf + (size_t)k * G.P;
       for (int p = lane; p < G.P; p += 64) {
-        cd z = cscale(Z[p], scale);
-        t[p] = conj ? cconj(z) : z;
+        const cd z = cscale(Z[p], scale);
+        o[p] = conj ? cconj(z) : z;
       }
       wave_sync();
     }
@@ -1274,6 +1308,46 @@ __global__ void __launch_bounds__(kBlock) apply_op_kernel(Geo G, int B, int tran
     row_inv<COOP>(G, D, spec, lds, [&](int r, int j, double v) { oi[r * G.W + j] = v; });
     __syncthreads();
   }
+}
+
+// A / AT for a few large images: three launches over many workgroups per
+// image (blockIdx.y = image): rows, columns x TF, inverse rows.
+template <bool COOP>
+__global__ void __launch_bounds__(kBlock) op_rows_kernel(Geo G, const double* x, cd* specws,
+                                                         size_t spec_stride) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cd* lds = reinterpret_cast<cd*>(smem);
+  const double* xi = x + (size_t)blockIdx.y * G.H * G.W;
+  Part D = solo_part(G.nfw);
+  D.gw0 = blockIdx.x * G.nfw;
+  D.gws = gridDim.x * G.nfw;
+  load_tw_lds(G);
+  row_fwd<COOP>(G, D, G.H, G.W, G.H, specws + blockIdx.y * spec_stride, lds,
+                [&](int r, int j) { return xi[r * G.W + j]; });
+}
+template <bool COOP>
+__global__ void __launch_bounds__(kBlock) op_cols_kernel(Geo G, int transpose, cd* specws,
+                                                         size_t spec_stride) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cd* lds = reinterpret_cast<cd*>(smem);
+  Part D = solo_part(G.nfw);
+  D.gw0 = blockIdx.x * G.nfw;
+  D.gws = gridDim.x * G.nfw;
+  load_tw_lds(G);
+  col_conv<COOP>(G, D, specws + blockIdx.y * spec_stride, tf_of(G, blockIdx.y, transpose), lds);
+}
+template <bool COOP>
+__global__ void __launch_bounds__(kBlock) op_rows_inv_kernel(Geo G, cd* specws,
+                                                             size_t spec_stride, double* out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  cd* lds = reinterpret_cast<cd*>(smem);
+  double* oi = out + (size_t)blockIdx.y * G.H * G.W;
+  Part D = solo_part(G.nfw);
+  D.gw0 = blockIdx.x * G.nfw;
+  D.gws = gridDim.x * G.nfw;
+  load_tw_lds(G);
+  row_inv<COOP>(G, D, specws + blockIdx.y * spec_stride, lds,
+                [&](int r, int j, double v) { oi[r * G.W + j] = v; });
 }
 
 // ----------------------------------------------------------- projectDF
@@ -1346,9 +1420,9 @@ hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s) {
 }
 template <bool COOP>
 static void launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
-  const dim3 grid(a.nimg * a.T), block(kBlock);
+  const dim3 grid(a.nimg * a.T), gcol(a.nimg * a.Tc), block(kBlock);
   hipLaunchKernelGGL((k_dir<COOP>), grid, block, lds, s, a);
-  hipLaunchKernelGGL((k_col<COOP>), grid, block, lds, s, a, 0);
+  hipLaunchKernelGGL((k_col<COOP>), gcol, block, lds, s, a, 0);
   // line-search kernel specialised on trial width, objective mode, adaptivity
   const bsgp_params& P = a.prm;
   const bool adapt = P.adapt_beta && P.variant == BSGP_VARIANT_BETA;
@@ -1375,7 +1449,7 @@ static void launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipStream_
   } else {
     hipLaunchKernelGGL((k_ls<2, -1, false, COOP>), grid, block, lds, s, a);
   }
-  hipLaunchKernelGGL((k_col<COOP>), grid, block, lds, s, a, 1);
+  hipLaunchKernelGGL((k_col<COOP>), gcol, block, lds, s, a, 1);
   hipLaunchKernelGGL((k_bb<COOP>), grid, block, lds, s, a);
 }
 hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
@@ -1389,11 +1463,28 @@ hipError_t launch_build_tf(const Geo& g, const double* kc, cd* spec, cd* tf, dou
                            int conj, size_t lds, hipStream_t s) {
   return launch_build_tfs(g, 1, kc, 0, spec, 0, tf, 0, scale, conj, lds, s);
 }
+// grid.x: workgroups per kernel grid, enough to cover the rows / columns
+// once the n grids share the device (the two launches are stream-ordered).
 hipError_t launch_build_tfs(const Geo& g, int n, const double* kc, size_t kc_stride, cd* spec,
                             size_t spec_stride, cd* tf, size_t tf_stride, double scale, int conj,
                             size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL(build_tf_kernel, dim3(n), dim3(kBlock), lds, s, g, kc, kc_stride, spec,
-                     spec_stride, tf, tf_stride, scale, conj);
+  const int slots = 1024;  // ~resident workgroups of the device
+  int per = slots / n;
+  if (per < 1) per = 1;
+  const int rp = (g.P + 1) / 2;  // row pairs
+  const int nr = (rp + g.nfw - 1) / g.nfw, nc = (g.Qh + g.nfw - 1) / g.nfw;
+  const dim3 gr(per < nr ? per : nr, n), gc(per < nc ? per : nc, n);
+  if (g.coop) {
+    hipLaunchKernelGGL((tf_rows_kernel<true>), gr, dim3(kBlock), lds, s, g, kc, kc_stride, spec,
+                       spec_stride);
+    hipLaunchKernelGGL((tf_cols_kernel<true>), gc, dim3(kBlock), lds, s, g, spec, spec_stride, tf,
+                       tf_stride, scale, conj);
+  } else {
+    hipLaunchKernelGGL((tf_rows_kernel<false>), gr, dim3(kBlock), lds, s, g, kc, kc_stride, spec,
+                       spec_stride);
+    hipLaunchKernelGGL((tf_cols_kernel<false>), gc, dim3(kBlock), lds, s, g, spec, spec_stride,
+                       tf, tf_stride, scale, conj);
+  }
   return hipGetLastError();
 }
 hipError_t launch_place_psfs(const Geo& g, int n, const double* psfs, int kh, int kw, int circ,
@@ -1410,6 +1501,28 @@ hipError_t launch_apply_op(const Geo& g, int B, int transpose, const double* x, 
   else
     hipLaunchKernelGGL((apply_op_kernel<false>), dim3(grid), dim3(kBlock), lds, s, g, B, transpose,
                        x, out, specws, spec_stride);
+  return hipGetLastError();
+}
+template <bool COOP>
+static void launch_apply_split_t(const Geo& g, int B, int transpose, const double* x, double* out,
+                                 cd* specws, size_t spec_stride, int per, size_t lds,
+                                 hipStream_t s) {
+  const int rp = (g.H + 1) / 2;
+  const int nr = (rp + g.nfw - 1) / g.nfw, nc = (g.Qh + g.nfw - 1) / g.nfw;
+  const dim3 gr(per < nr ? per : nr, B), gc(per < nc ? per : nc, B);
+  hipLaunchKernelGGL((op_rows_kernel<COOP>), gr, dim3(kBlock), lds, s, g, x, specws, spec_stride);
+  hipLaunchKernelGGL((op_cols_kernel<COOP>), gc, dim3(kBlock), lds, s, g, transpose, specws,
+                     spec_stride);
+  hipLaunchKernelGGL((op_rows_inv_kernel<COOP>), gr, dim3(kBlock), lds, s, g, specws,
+                     spec_stride, out);
+}
+hipError_t launch_apply_op_split(const Geo& g, int B, int transpose, const double* x,
+                                 double* out, cd* specws, size_t spec_stride, int per, size_t lds,
+                                 hipStream_t s) {
+  if (g.coop)
+    launch_apply_split_t<true>(g, B, transpose, x, out, specws, spec_stride, per, lds, s);
+  else
+    launch_apply_split_t<false>(g, B, transpose, x, out, specws, spec_stride, per, lds, s);
   return hipGetLastError();
 }
 hipError_t launch_project_df(int n, double b, const double* c, const double* dia, ProjClip clip,
@@ -1465,7 +1578,11 @@ hipError_t set_solver_lds_limit(size_t bytes) {
                        (const void*)k_ls<2, -1, false, true>,
                        (const void*)k_bb<true>,
                        (const void*)apply_op_kernel<true>,
-                       (const void*)build_tf_kernel};
+                       (const void*)tf_rows_kernel<false>, (const void*)tf_rows_kernel<true>,
+                       (const void*)tf_cols_kernel<false>, (const void*)tf_cols_kernel<true>,
+                       (const void*)op_rows_kernel<false>, (const void*)op_rows_kernel<true>,
+                       (const void*)op_cols_kernel<false>, (const void*)op_cols_kernel<true>,
+                       (const void*)op_rows_inv_kernel<false>, (const void*)op_rows_inv_kernel<true>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return e;
