@@ -61,6 +61,41 @@ def test_linear_operator_matches_astropy(B):
         assert rel(at, fx[f"AT{i}"]) < 1e-12, (i, rel(at, fx[f"AT{i}"]))
 
 
+@pytest.mark.parametrize("linear", [True, False])
+def test_operator_split_and_persistent_paths_agree(B, linear):
+    """bsgp_apply_operator spreads few images over many workgroups (rows,
+    columns, rows) and runs one persistent workgroup per image for many: the
+    same transforms, so the same bits."""
+    import cpu_bench
+    psf = cpu_bench.gaussian_psf(25) if linear else np.fft.ifftshift(
+        np.pad(cpu_bench.gaussian_psf(25), ((52, 51), (52, 51))))
+    mode = B.BSGP_CONV_LINEAR_FILL if linear else B.BSGP_CONV_CIRCULAR
+    plan = B.get_plan(128, 128, psf, mode)
+    rng = np.random.default_rng(3)
+    x = B.to_dev(rng.uniform(0, 1, (300, 128, 128)))  # 300 * 4 > 1024 slots: persistent
+    for tr in (False, True):
+        many = plan.apply(x, transpose=tr).cpu().numpy()
+        for i in (0, 137, 299):
+            one = plan.apply(x[i:i + 1].contiguous(), transpose=tr).cpu().numpy()[0]
+            np.testing.assert_array_equal(one, many[i])
+
+
+def test_operator_2048_matches_numpy(B):
+    """One 2048x2048 image: cooperative (workgroup-wide) transforms, TF built
+    over many workgroups, A/AT against numpy."""
+    rng = np.random.default_rng(4)
+    psf = np.zeros((2048, 2048))
+    psf[1024 - 32:1024 + 32, 1024 - 32:1024 + 32] = rng.uniform(0, 1, (64, 64))
+    psf /= psf.sum()
+    plan = B.get_plan(2048, 2048, psf, B.BSGP_CONV_CIRCULAR)
+    x = rng.uniform(0, 1, (2048, 2048))
+    TF = np.fft.rfft2(np.fft.fftshift(psf))
+    for tr in (False, True):
+        out = plan.apply(B.to_dev(x[None]), transpose=tr).cpu().numpy()[0]
+        ref = np.fft.irfft2((np.conj(TF) if tr else TF) * np.fft.rfft2(x), s=x.shape)
+        assert rel(out, ref) < 1e-13
+
+
 def test_odd_circular_operator_fftshift_quirk(B):
     """31x31: fftshift puts the PSF centre at n-1."""
     psf = np.zeros((31, 31))
