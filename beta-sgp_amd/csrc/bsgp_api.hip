@@ -527,6 +527,7 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     const int want = 4 * p->ncu / B;
     a.Tc = std::max(T, std::min(nc, want));
   }
+  a.fuse_col = T == 1 ? BSGP_FUSE_COL : 0;
   a.tpart = T > 1 ? p->tpart : nullptr;
   a.tctr = p->tctr;
   a.tfail = reinterpret_cast<int*>(p->tctr + B);

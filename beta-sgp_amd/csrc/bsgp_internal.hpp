@@ -24,6 +24,15 @@ struct ImgState {
 
 // Everything a phase kernel needs (passed by value: kernel-argument loads are
 // scalar, so plan geometry and pointers stay in SGPRs).
+// Column passes run inside the phase kernels for one-workgroup images
+// instead of as k_col launches: A's at the end of k_dir (bit 0) or at the
+// start of k_ls (bit 2), AT's at the end of k_ls (bit 1).  Measured on C3
+// (A/B): AT's in k_ls +4.5 %; A's in k_dir -25 % (252 VGPRs + scratch: the
+// projection state stays live), A's also in k_ls -1 % (spills at 168 VGPRs).
+#ifndef BSGP_FUSE_COL
+#define BSGP_FUSE_COL 2
+#endif
+
 struct SolveArgs {
   Geo g;
   bsgp_params prm;
@@ -40,6 +49,7 @@ struct SolveArgs {
   // teams (T workgroups per image; T = 1: one workgroup, none of these used)
   int T;
   int Tc;               // workgroups per image of k_col (no reductions there: not a team)
+  int fuse_col;         // T == 1: BSGP_FUSE_COL (which phase kernels run the column passes)
   double* tpart;        // [B][2][T][kMaxRed] reduction partials
   unsigned int* tctr;   // [B] barrier arrival counters, zeroed per solve
   int* tfail;           // set by a timed-out barrier spin

@@ -478,7 +478,10 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
 // bound (for the convex sum the secant and Newton iterates fall on either
 // side of the root); on later misses, the tightest bracket of signs seen.
 // A miss is just a full pass, so the choice of bracket never changes results.
-constexpr double kProjGuessW = 0.3;
+#ifndef BSGP_PROJ_GUESS_W
+#define BSGP_PROJ_GUESS_W 0.3
+#endif
+constexpr double kProjGuessW = BSGP_PROJ_GUESS_W;
 
 __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt, Team& tm,
                                      const Dir& D, const Bufs& B, double* red, double lam_prev,
@@ -728,6 +731,12 @@ __global__ void __launch_bounds__(kBlock) BSGP_DIR_ATTR k_dir(SolveArgs A) {
       });
   team_sum<1>(gd, red, tm);
   PH_ADD(1, tk1);
+  if ((BSGP_FUSE_COL & 1) && (A.fuse_col & 1)) {  // T == 1: A's column pass follows here
+    PH_T(tc0);
+    team_sync(tm);
+    col_conv<COOP>(G, Pt, B.spec, tf_of(G, img, 0), lds);
+    PH_ADD(3, tc0);
+  }
   PH_ADD(2, tk0);
   team_end(st, tm);
   if (leader(tm)) {  // sgp.py:306-308 (memory shifts) + direction scalars
@@ -787,6 +796,12 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   const double lr_st = st.lr;
   constexpr bool adapt = ADAPT;  // adaptive beta (sgp.py:798-800): K == 1, runtime mode
   Bufs B = slot_bufs(A, img, st.par);
+  if ((BSGP_FUSE_COL & 4) && (A.fuse_col & 4)) {  // T == 1: A's column pass of k_dir's rows
+    PH_T(tc0);
+    col_conv<COOP>(G, Pt, B.spec, tf_of(G, img, 0), lds);
+    team_sync(tm);
+    PH_ADD(3, tc0);
+  }
   const double bks_scalar = st.bks_scalar;
   const double flux = st.flux;
   const double gd = st.gd;
@@ -1016,6 +1031,12 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
         return g * (p / den);
       });
   PH_ADD(6, tk2);
+  if ((BSGP_FUSE_COL & 2) && (A.fuse_col & 2)) {  // T == 1: AT's column pass follows here
+    PH_T(tc0);
+    team_sync(tm);
+    col_conv<COOP>(G, Pt, B.spec, tf_of(G, img, 1), lds);
+    PH_ADD(3, tc0);
+  }
   PH_ADD(7, tk0);
   team_end(st, tm);
   if (leader(tm)) {
@@ -1422,7 +1443,7 @@ template <bool COOP>
 static void launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
   const dim3 grid(a.nimg * a.T), gcol(a.nimg * a.Tc), block(kBlock);
   hipLaunchKernelGGL((k_dir<COOP>), grid, block, lds, s, a);
-  hipLaunchKernelGGL((k_col<COOP>), gcol, block, lds, s, a, 0);
+  if (!(a.fuse_col & 5)) hipLaunchKernelGGL((k_col<COOP>), gcol, block, lds, s, a, 0);
   // line-search kernel specialised on trial width, objective mode, adaptivity
   const bsgp_params& P = a.prm;
   const bool adapt = P.adapt_beta && P.variant == BSGP_VARIANT_BETA;
@@ -1449,7 +1470,7 @@ static void launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipStream_
   } else {
     hipLaunchKernelGGL((k_ls<2, -1, false, COOP>), grid, block, lds, s, a);
   }
-  hipLaunchKernelGGL((k_col<COOP>), gcol, block, lds, s, a, 1);
+  if (!(a.fuse_col & 2)) hipLaunchKernelGGL((k_col<COOP>), gcol, block, lds, s, a, 1);
   hipLaunchKernelGGL((k_bb<COOP>), grid, block, lds, s, a);
 }
 hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
