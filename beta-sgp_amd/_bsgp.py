@@ -52,6 +52,7 @@ class Params(ctypes.Structure):
         ("adapt_beta", ctypes.c_int32), ("schedule_lr", ctypes.c_int32),
         ("bkg_is_map", ctypes.c_int32), ("ls_spec", ctypes.c_int32), ("ls_series", ctypes.c_int32),
         ("streams", ctypes.c_int32), ("team", ctypes.c_int32), ("proj_cache", ctypes.c_int32),
+        ("gn_compact", ctypes.c_int32),
     ]
 
 

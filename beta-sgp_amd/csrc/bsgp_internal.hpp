@@ -18,6 +18,11 @@ struct ImgState {
   double sc, flux, bks_scalar, lo, hi, Dcoeff, tol, t0;
   double fv, alpha, tau, lr, init_lr, beta, lam_p, gd, lam;
   double konst;  // lambda-independent objective sum at `beta` (sum s*gn^b / sum gn)
+  // compact observed image (params.gn_compact): 0 = gn_s stored in f64; 1 = the
+  // raw counts stored in f32, gn_s = raw (scale_data 0/2); 2 = gn_s = raw / sc.
+  // gfill is the null-pixel value vmin*eps^2 (sgp.py:202-204).
+  int g32;
+  double gfill;
   double Valpha[32];
   double Fold[32];
 };

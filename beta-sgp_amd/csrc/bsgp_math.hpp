@@ -87,6 +87,19 @@ BSGP_HD double fast_exp(double t) {
   return std::ldexp(1.0 + p, (int)kd);
 }
 
+// a / b correctly rounded from r = RN(1/b) (Markstein's final correction step,
+// the one IA-64 division ends with): q = RN(a*r) is within an ulp of a/b, the
+// residual a - b*q is exact by fma, and RN(q + residual*r) is the correctly
+// rounded quotient when nothing over/underflows.  For the compact gn decode
+// (positive f32 counts over a positive f32 scaling) that always holds; it
+// needs 3 fp64 ops and no temporaries of v_div_scale/v_div_fixup.  Checked
+// bit for bit against a / b in tests/cpp/math_test.cpp.
+BSGP_HD double div_rn(double a, double b, double r) {
+  const double q = a * r;
+  const double e = std::fma(-q, b, a);
+  return std::fma(e, r, q);
+}
+
 // x**a for positive x via exp(a*log x); for |a*log x| small (the beta-1
 // exponents of this path) the result carries ~1 ulp.
 BSGP_HD double fast_pow(double x, double a) { return fast_exp(a * fast_log(x)); }

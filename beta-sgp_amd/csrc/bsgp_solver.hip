@@ -297,15 +297,18 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   // raw statistics (sgp.py:174-177, 190, 193-194)
   double v2[2] = {0.0, 0.0};  // sum(gn - bkg), sum(gn)
   double mx = -INFINITY;
+  double ok32 = 1.0;  // every raw value finite and exact in f32 (params.gn_compact)
   for (int i = D.gt0 + tid; i < N; i += D.gts) {
     const double g = gn_in[i];
     const double bkr = bmap ? bk_in[i] : bk_scalar_raw;
     v2[0] += g - bkr;
     v2[1] += g;
     mx = (g > mx || g != g) ? g : mx;
+    if (!(isfinite(g) && (double)(float)g == g)) ok32 = 0.0;
   }
   team_sum<2>(v2, red, tm);
   mx = team_max(mx, red, tm);
+  if (P.gn_compact) ok32 = team_min(ok32, red, tm);
   const double sc = P.scale_data == 2 ? P.prescaled_scaling : (P.scale_data ? mx : 1.0);
   const double fl_raw = A.in.flux ? A.in.flux[img] : v2[0];
   const double x3 = (fl_raw / (double)N) * 1.0;  // np.sum(gn-bkg)/gn.size*ones (sgp.py:175)
@@ -419,6 +422,16 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     lo = lo / 10;
     hi = hi * 10;
   }
+  // Compact observed image: the raw f32-exact values replace gn_s in the first
+  // half of its slot vector (every f64 read of gn_s is done: team_sync above).
+  // Readers recompute gn_s = raw / sc (or raw), and the null-pixel fill for
+  // raw <= 0, with the operations used above: the same bits as f64 storage.
+  const int g32 = (P.gn_compact && ok32 > 0.5) ? (divide ? (sc > 0 ? 2 : 0) : 1) : 0;
+  if (g32) {
+    float* gf = reinterpret_cast<float*>(B.gns);
+    for (int i = D.gt0 + tid; i < N; i += D.gts) gf[i] = (float)gn_in[i];
+    if (odd && leader(tm)) gf[N] = 1.0f;  // pad element of the pair-vectorised streams
+  }
   const double Dcoeff = 2 / (double)N * sc;
   double tol = P.tol_convergence;
   if (P.stop_criterion == 4) tol = tol4;
@@ -455,6 +468,8 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     st.init_lr = P.lr;
     st.beta = beta0;
     st.konst = fsum[0];
+    st.g32 = g32;
+    st.gfill = fill;
     atomicAdd(A.active, 1);
   }
 }
@@ -805,6 +820,22 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   const double bks_scalar = st.bks_scalar;
   const double flux = st.flux;
   const double gd = st.gd;
+  // compact gn (ImgState::g32): loaders fetch the raw f32, users decode it
+  const int g32 = st.g32;
+  const double gsc = st.sc, grc = 1.0 / st.sc, gfill = st.gfill;
+  const float* gnf = reinterpret_cast<const float*>(B.gns);
+  // (the raw f32 travels in the low word of the f64 operand register, so both
+  // storage modes use the same registers)
+  auto gdec1 = [&](float v) __attribute__((always_inline)) {
+    const double g = v;
+    return g > 0 ? (g32 == 2 ? div_rn(g, gsc, grc) : g) : gfill;
+  };
+  auto gdec = [&](double r) __attribute__((always_inline)) {
+    return g32 ? gdec1(__int_as_float(__double2loint(r))) : r;
+  };
+  auto gload = [&](int i) __attribute__((always_inline)) {
+    return g32 ? __hiloint2double(0, __float_as_int(gnf[i])) : B.gns[i];
+  };
   double fr = st.Fold[0];
   for (int k = 1; k < P.M; ++k) fr = py_max2(fr, st.Fold[k]);
   Objective obj = make_obj(A, st.beta);
@@ -843,7 +874,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
           const int i = r * G.W + j;
           LsIn q;
           q.x0 = B.xtf[i];
-          q.g = B.gns[i];
+          q.g = gload(i);
           q.p0 = series ? B.pw[i] : 0.0;
           q.bkv = bmap ? B.bks[i] : bks_scalar;
           return q;
@@ -851,7 +882,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
         [&](int r, int j, double v, const LsIn& q) {
       const int i = r * G.W + j;
       B.dtf[i] = v;
-      const double g = q.g;
+      const double g = gdec(q.g);
       const double x0 = q.x0;
       const double bkv = q.bkv;
       const double xt = x0 + lam * v;
@@ -967,13 +998,24 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
           } v;
           v.x = ld2(xtf, p);
           v.d = ld2(dtf, p);
-          v.g = ld2(gns, p);
+          if (g32) {  // the pair's two f32 in the first f64 slot
+            v.g.x = __longlong_as_double(reinterpret_cast<const long long*>(gnf)[p]);
+            v.g.y = 0.0;
+          } else {
+            v.g = ld2(gns, p);
+          }
           v.b = bmap ? ld2(bks, p) : double2{bks_scalar, bks_scalar};
           return v;
         },
         [&](int p, const auto& v) {
-          eval_px(v.x.x, v.d.x, v.g.x, v.b.x);
-          if (!odd || 2 * p + 1 < N) eval_px(v.x.y, v.d.y, v.g.y, v.b.y);
+          double g0 = v.g.x, g1 = v.g.y;
+          if (g32) {
+            const long long w = __double_as_longlong(v.g.x);
+            g0 = gdec1(__int_as_float((int)(w & 0xffffffffLL)));
+            g1 = gdec1(__int_as_float((int)(w >> 32)));
+          }
+          eval_px(v.x.x, v.d.x, g0, v.b.x);
+          if (!odd || 2 * p + 1 < N) eval_px(v.x.y, v.d.y, g1, v.b.y);
         });
     team_sum<NT>(t, red, tm);
     if (adapt) konst = t[2 * K];
@@ -1015,7 +1057,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
         AcIn q;
         q.x = B.xtf[i];
         q.d = B.dtf[i];
-        q.g = B.gns[i];
+        q.g = gload(i);
         q.bkv = bmap ? B.bks[i] : bks_scalar;
         return q;
       },
@@ -1024,7 +1066,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
         const double xt = q.x + lam_acc * q.d;
         B.xtf[i] = xt;
         const double den = xt + q.bkv;
-        const double g = q.g;
+        const double g = gdec(q.g);
         if (P.variant != BSGP_VARIANT_BETA) return g / den;  // KL: w = gn/den
         const double p = fpow(den, obj.beta - 1);
         B.pw[i] = p;

@@ -48,6 +48,7 @@ LS_SERIES_DEFAULT = 1  # small line-search steps from the moment series (general
 STREAMS_DEFAULT = 3  # sub-batch streams of a batched solve (+ the caller's = 4 HW queues; 4 sub-streams collapse under the default GPU_MAX_HW_QUEUES=4)
 TEAM_DEFAULT = 0  # workgroups per image: 0 = auto (spread small batches over the CUs)
 PROJ_CACHE_DEFAULT = 1  # projectDF evaluations inside a known root bracket read a pixel list
+GN_COMPACT_DEFAULT = 1  # f32-exact observed images stored in f32 (bit-identical results)
 
 
 # ------------------------------------------------------------------ helpers
@@ -101,7 +102,7 @@ def _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, 
             alpha_max, M_alpha, tau, M, max_projs, verbose, ccd_sat_level, scale_data,
             tol_convergence, adapt_beta=False, betaParam=1.005, lr=1e-3, lr_exp_param=0.1,
             schedule_lr=False, bkg_is_map=False, ls_spec=None, ls_series=None, streams=None,
-            team=None, proj_cache=None):
+            team=None, proj_cache=None, gn_compact=None):
     p = _B.Params()
     p.variant = variant
     p.init_recon = int(init_recon)
@@ -128,6 +129,7 @@ def _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, 
     p.streams = STREAMS_DEFAULT if streams is None else int(streams)
     p.team = TEAM_DEFAULT if team is None else int(team)
     p.proj_cache = PROJ_CACHE_DEFAULT if proj_cache is None else int(bool(proj_cache))
+    p.gn_compact = GN_COMPACT_DEFAULT if gn_compact is None else int(bool(gn_compact))
     return p
 
 
@@ -300,7 +302,8 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
                  ccd_sat_level=None, scale_data=True, tol_convergence=1e-4,
                  use_original_SGP_Afunction=True, adapt_beta=False, betaParam=1.005, lr=1e-3,
                  lr_exp_param=0.1, schedule_lr=False, ls_spec=None, ls_series=None,
-                 streams=None, team=None, proj_cache=None, device_out=False):
+                 streams=None, team=None, proj_cache=None, gn_compact=None,
+                 device_out=False):
     torch = _B.torch
     per_image = (psf.dim() if torch.is_tensor(psf) else np.ndim(psf)) == 3
     if not per_image:
@@ -320,7 +323,7 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
                   scale_data, tol_convergence, adapt_beta=adapt_beta, betaParam=betaParam, lr=lr,
                   lr_exp_param=lr_exp_param, schedule_lr=schedule_lr, bkg_is_map=bkg_is_map,
                   ls_spec=ls_spec, ls_series=ls_series, streams=streams,
-                  team=team, proj_cache=proj_cache)
+                  team=team, proj_cache=proj_cache, gn_compact=gn_compact)
     x0 = None
     if init_recon == 1:
         np.random.seed(42)

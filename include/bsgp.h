@@ -84,6 +84,11 @@ typedef struct {
                              bracket known to hold the root read only the pixels that
                              change state inside it (a per-lane list written by the
                              last full pass); 0: every evaluation streams the image */
+  int32_t gn_compact;     /* 1: an image whose observed values are all finite and exact
+                             in f32 (counts, or f32 FITS data) keeps them in f32 and
+                             recomputes the scaled gn/scaling (and the null-pixel fill)
+                             on every read, bit-identical to f64 storage; the line
+                             search reads half the bytes of gn. 0: f64 storage */
 } bsgp_params;
 
 /* Device inputs of a batched solve. */
