@@ -25,6 +25,12 @@ BSGP_CONV_CIRCULAR = 0
 BSGP_CONV_LINEAR_FILL = 1
 BSGP_VARIANT_KL = 0
 BSGP_VARIANT_BETA = 1
+BSGP_STORAGE_F64 = 0
+BSGP_STORAGE_F32 = 1
+ABI_VERSION = 2
+BSGP_ERR_ARG = -1
+BSGP_ERR_HIP = -2
+BSGP_ERR_UNSUPPORTED = -3
 BSGP_ERR_PSF = -4
 
 
@@ -52,7 +58,8 @@ class Params(ctypes.Structure):
         ("adapt_beta", ctypes.c_int32), ("schedule_lr", ctypes.c_int32),
         ("bkg_is_map", ctypes.c_int32), ("ls_spec", ctypes.c_int32), ("ls_series", ctypes.c_int32),
         ("streams", ctypes.c_int32), ("team", ctypes.c_int32), ("proj_cache", ctypes.c_int32),
-        ("gn_compact", ctypes.c_int32),
+        ("gn_compact", ctypes.c_int32), ("gn_f32", ctypes.c_int32),
+        ("beta0_general", ctypes.c_int32),
     ]
 
 
@@ -60,12 +67,13 @@ _P = ctypes.c_void_p
 
 
 class Inputs(ctypes.Structure):
-    _fields_ = [("gn", _P), ("bkg", _P), ("flux", _P), ("x0", _P), ("beta0", _P)]
+    _fields_ = [("gn", _P), ("bkg", _P), ("flux", _P), ("x0", _P), ("beta0", _P), ("obj", _P)]
 
 
 class Outputs(ctypes.Structure):
     _fields_ = [("x", _P), ("iters", _P), ("discr", _P), ("times", _P), ("crit", _P),
-                ("flags", _P), ("beta_final", _P), ("counters", _P)]
+                ("flags", _P), ("beta_final", _P), ("counters", _P), ("err", _P),
+                ("x_iter", _P)]
 
 
 class PsfModel(ctypes.Structure):
@@ -94,7 +102,7 @@ def lib():
             i32, i64, dbl, vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
             L.bsgp_last_error.restype = ctypes.c_char_p
             L.bsgp_abi_version.restype = i32
-            L.bsgp_plan_create.argtypes = [i32, i32, vp, i32, i32, i32, i32,
+            L.bsgp_plan_create.argtypes = [i32, i32, vp, i32, i32, i32, i32, i32,
                                            ctypes.POINTER(vp)]
             L.bsgp_plan_destroy.argtypes = [vp]
             L.bsgp_plan_info.argtypes = [vp, vp, vp, vp, vp]
@@ -118,6 +126,9 @@ def lib():
                          "bsgp_extract_tiles", "bsgp_coadd_tiles", "bsgp_fits_to_f64",
                          "bsgp_psf_stamps", "bsgp_plan_set_psfs"]:
                 getattr(L, name).restype = ctypes.c_int
+            if L.bsgp_abi_version() != ABI_VERSION:
+                raise BsgpError(-3, f"{LIB_PATH} has ABI {L.bsgp_abi_version()}, this binding "
+                                    f"needs {ABI_VERSION}: rebuild with __graft_entry__.build()")
             _lib = L
     return _lib
 
@@ -151,7 +162,7 @@ def current_stream():
 class Plan:
     """A device plan: FFT geometry + PSF transfer functions (bsgp_plan_create)."""
 
-    def __init__(self, H, W, psf, conv_mode, device=None):
+    def __init__(self, H, W, psf, conv_mode, device=None, storage=BSGP_STORAGE_F64):
         require_gpu()
         if device is None:
             device = torch.cuda.current_device()
@@ -160,9 +171,10 @@ class Plan:
         self.kh, self.kw = psf.shape
         self.conv_mode = conv_mode
         self.device = device
+        self.storage = storage
         h = ctypes.c_void_p()
         rc = lib().bsgp_plan_create(self.H, self.W, psf.ctypes.data, self.kh, self.kw, conv_mode,
-                                    device, ctypes.byref(h))
+                                    storage, device, ctypes.byref(h))
         if rc != 0:
             raise BsgpError(rc, lib().bsgp_last_error().decode(errors="replace"))
         self.h = h
@@ -202,10 +214,13 @@ class Plan:
         return out
 
     # ------------------------------------------------------------------ solve
-    def solve(self, gn, bkg, params, flux=None, x0=None, beta0=None, want_times=True):
+    def solve(self, gn, bkg, params, flux=None, x0=None, beta0=None, want_times=True, obj=None,
+              want_iterates=False):
         """Batched solve on device tensors: gn [B,H,W] f64; bkg [B] or [B,H,W];
-        flux/beta0 [B] or None; x0 [B,H,W] or None.  Asynchronous on the
-        current stream; returns a dict of device output tensors."""
+        flux/beta0 [B] or None; x0 [B,H,W] or None; obj [B,H,W] or None (then
+        "err" holds the per-iteration relative error); want_iterates adds
+        "x_iter" [B,MAXIT,H,W].  Asynchronous on the current stream; returns a
+        dict of device output tensors."""
         B = gn.shape[0]
         M1 = params.MAXIT + 1
         dev = gn.device
@@ -219,25 +234,36 @@ class Plan:
             "flags": torch.zeros(B, M1, dtype=torch.int32, device=dev),
             "beta_final": torch.zeros(B, **f64),
             "counters": torch.zeros(B, 8, dtype=torch.int64, device=dev),
+            "err": torch.zeros(B, M1, **f64) if obj is not None else None,
+            "x_iter": (torch.zeros(B, params.MAXIT, self.H, self.W, **f64) if want_iterates
+                       else None),
         }
-        ins = Inputs(_ptr(gn), _ptr(bkg), _ptr(flux), _ptr(x0), _ptr(beta0))
+        ins = Inputs(_ptr(gn), _ptr(bkg), _ptr(flux), _ptr(x0), _ptr(beta0), _ptr(obj))
         outs = Outputs(*[_ptr(out[k]) for k in ["x", "iters", "discr", "times", "crit", "flags",
-                                                 "beta_final", "counters"]])
-        self._keep = (gn, bkg, flux, x0, beta0)
+                                                 "beta_final", "counters", "err", "x_iter"]])
+        self._keep = (gn, bkg, flux, x0, beta0, obj)
         check(lib().bsgp_solve_device(self.h, B, ctypes.byref(params), ctypes.byref(ins),
                                       ctypes.byref(outs), current_stream()))
         return out
 
 
+STATUS_LS_CAP = 1
 STATUS_TEAM_TIMEOUT = 4
 
 
 def check_status(counters):
-    """Raise if a solve reported a team-barrier timeout (counters[:, 3] bit 4):
-    its results are not valid."""
-    st = counters[:, 3].cpu().numpy()
+    """Raise if a solve reported a status bit in counters[:, 3]: its results
+    are not valid.  Bit 1: the line search hit its trial cap, which happens
+    only for a backtracking factor outside (0, 1), where the reference's
+    loop (sgp.py:328-349 / 776-801) never terminates; bit 4: a team barrier
+    timed out (workgroups not co-resident)."""
+    c = counters.cpu().numpy() if hasattr(counters, "cpu") else np.asarray(counters)
+    st = c[:, 3]
     if np.any(st & STATUS_TEAM_TIMEOUT):
         raise BsgpError(BSGP_ERR_HIP, "team barrier timed out (workgroups not co-resident)")
+    if np.any(st & STATUS_LS_CAP):
+        raise BsgpError(BSGP_ERR_ARG, "line search did not terminate: the backtracking factor "
+                                      "beta must lie in (0, 1) (sgp.py:349 lam = lam * beta)")
 
 
 _plan_cache = {}
@@ -245,11 +271,13 @@ _plan_cache_lock = threading.Lock()
 
 
 def get_plan(H, W, psf, conv_mode):
-    """Plans are cached per (shape, psf bytes, mode, device)."""
+    """Plans are cached per (shape, psf bytes, mode, device, host thread): a
+    plan's workspace belongs to one solve at a time (include/bsgp.h: one plan
+    per device per host thread), so threads never share one."""
     require_gpu()
     psf = np.ascontiguousarray(psf, dtype="<f8")
     dev = torch.cuda.current_device()
-    key = (H, W, psf.shape, psf.tobytes(), conv_mode, dev)
+    key = (H, W, psf.shape, psf.tobytes(), conv_mode, dev, threading.get_ident())
     with _plan_cache_lock:
         p = _plan_cache.get(key)
         if p is None:

@@ -35,6 +35,72 @@ int fail(int code, const std::string& msg) {
 
 size_t round_up(size_t v, size_t m) { return (v + m - 1) / m * m; }
 
+// numpy's float32 np.sum over n contiguous elements (numpy 1.26 and 2.x,
+// checked against np.sum in tests/test_oracle.py::test_numpy_f32_sum_model):
+// the reduction runs over chunks of 8192 (the ufunc buffer), folding
+// res = res + pairwise(chunk) from res = 0; pairwise(n) is a leaf for n <= 128
+// (8 strided accumulators, or a plain loop below 8) and otherwise
+// pairwise(n2) + pairwise(n - n2) with n2 = n/2 - (n/2) % 8.  The program
+// lists the leaves (start, length) in order, the inner nodes (value indices
+// of the two operands; values 0..L-1 are the leaves, L+k is node k) grouped
+// by height so that a level can be added in parallel, and each chunk's root.
+struct PwBuild {
+  std::vector<int> leaves, nodes_tmp, heights, roots;
+  // returns a temporary id: >= 0 leaf, < 0 node -(k+1); *h = height
+  int rec(int start, int n, int* h) {
+    if (n <= 128) {
+      leaves.push_back(start);
+      leaves.push_back(n);
+      *h = 0;
+      return (int)leaves.size() / 2 - 1;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    int ha, hb;
+    const int a = rec(start, n2, &ha);
+    const int b = rec(start + n2, n - n2, &hb);
+    nodes_tmp.push_back(a);
+    nodes_tmp.push_back(b);
+    *h = (ha > hb ? ha : hb) + 1;
+    heights.push_back(*h);
+    return -(int)(nodes_tmp.size() / 2);
+  }
+};
+
+std::vector<int> pairwise_program(long n, PwProg* pp) {
+  PwBuild b;
+  std::vector<int> root_tmp;
+  for (long c0 = 0; c0 < n; c0 += 8192) {
+    int h;
+    root_tmp.push_back(b.rec((int)c0, (int)std::min<long>(8192, n - c0), &h));
+  }
+  const int L = (int)b.leaves.size() / 2, M = (int)b.heights.size();
+  int maxh = 0;
+  for (int v : b.heights) maxh = std::max(maxh, v);
+  // order the nodes by height (stable), then renumber the operands
+  std::vector<int> order, newid(M), lev_off(maxh + 1, 0);
+  for (int h = 1; h <= maxh; ++h) {
+    lev_off[h - 1] = (int)order.size();
+    for (int k = 0; k < M; ++k)
+      if (b.heights[k] == h) order.push_back(k);
+  }
+  lev_off[maxh] = (int)order.size();
+  for (int i = 0; i < M; ++i) newid[order[i]] = L + i;
+  auto val = [&](int t) { return t >= 0 ? t : newid[-t - 1]; };
+  std::vector<int> prog(b.leaves);
+  for (int i = 0; i < M; ++i) {
+    prog.push_back(val(b.nodes_tmp[2 * order[i]]));
+    prog.push_back(val(b.nodes_tmp[2 * order[i] + 1]));
+  }
+  for (int v : lev_off) prog.push_back(v);
+  for (int t : root_tmp) prog.push_back(val(t));
+  pp->nleaf = L;
+  pp->nnode = M;
+  pp->nlev = maxh;
+  pp->nchunk = (int)root_tmp.size();
+  return prog;
+}
+
 std::vector<cd> twiddles(int n) {
   std::vector<cd> t(n);
   const long double pi = 3.141592653589793238462643383279502884L;
@@ -85,6 +151,10 @@ struct bsgp_plan_s {
   // operator workspace
   cd* opws = nullptr;
   size_t opws_slots = 0;
+  int storage = BSGP_STORAGE_F64;
+  // numpy's float32 reduction order over N elements (gn_f32 solves)
+  int* pwprog = nullptr;
+  PwProg pw{};
 };
 
 // Capacity of one thread's projection list: the pixels it streams in one pass
@@ -170,7 +240,7 @@ static int ensure_team(bsgp_plan p, size_t B, int T) {
 
 extern "C" {
 
-int32_t bsgp_abi_version(void) { return 1; }
+int32_t bsgp_abi_version(void) { return 2; }
 
 // Diagnostics (not in include/bsgp.h): per-phase shader cycles of a build
 // with -DBSGP_PHASE_PROF; returns BSGP_ERR_UNSUPPORTED otherwise.
@@ -181,6 +251,24 @@ int bsgp_phase_prof(uint64_t* out, int32_t n, int32_t reset) {
   return BSGP_OK;
 }
 
+// Diagnostics (not in include/bsgp.h): the numpy float32 reduction program the
+// plans use for N = n elements (tests/test_oracle.py evaluates it against
+// np.sum).  counts = {nleaf, nnode, nlev, nchunk}; returns the program length,
+// copying at most cap ints to out.
+int64_t bsgp_pairwise_program(int64_t n, int32_t* out, int64_t cap, int32_t* counts) {
+  if (n < 1) return fail(BSGP_ERR_ARG, "n must be >= 1");
+  PwProg pp{};
+  const std::vector<int> prog = pairwise_program((long)n, &pp);
+  if (counts) {
+    counts[0] = pp.nleaf;
+    counts[1] = pp.nnode;
+    counts[2] = pp.nlev;
+    counts[3] = pp.nchunk;
+  }
+  for (int64_t i = 0; out && i < cap && i < (int64_t)prog.size(); ++i) out[i] = prog[i];
+  return (int64_t)prog.size();
+}
+
 const char* bsgp_last_error(void) { return g_err.c_str(); }
 
 int bsgp_device_synchronize(void) {
@@ -189,8 +277,10 @@ int bsgp_device_synchronize(void) {
 }
 
 int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_t kw,
-                     int32_t conv_mode, int32_t device, bsgp_plan* out) {
+                     int32_t conv_mode, int32_t storage, int32_t device, bsgp_plan* out) {
   if (!out) return fail(BSGP_ERR_ARG, "out is NULL");
+  if (storage != BSGP_STORAGE_F64 && storage != BSGP_STORAGE_F32)
+    return fail(BSGP_ERR_ARG, "bad storage");
   *out = nullptr;
   if (H < 1 || W < 1 || kh < 1 || kw < 1 || !psf) return fail(BSGP_ERR_ARG, "bad shape or psf");
   if (conv_mode != BSGP_CONV_CIRCULAR && conv_mode != BSGP_CONV_LINEAR_FILL)
@@ -363,8 +453,23 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
     return fail(rc, m);
   }
   const size_t N = (size_t)H * W;
+  p->storage = storage;
+  if (storage == BSGP_STORAGE_F32) {
+    bsgp_plan_destroy(p);
+    return fail(BSGP_ERR_UNSUPPORTED, "float32 storage is not built yet");
+  }
   p->vec_stride = round_up(N, 32);
   p->slot_stride = 9 * p->vec_stride + round_up((size_t)H * g.Qh * 2, 32);
+  {
+    const std::vector<int> prog = pairwise_program((long)N, &p->pw);
+    if (hipMalloc(&p->pwprog, prog.size() * sizeof(int)) != hipSuccess ||
+        hipMemcpy(p->pwprog, prog.data(), prog.size() * sizeof(int), hipMemcpyHostToDevice) !=
+            hipSuccess) {
+      bsgp_plan_destroy(p);
+      return fail(BSGP_ERR_HIP, "pairwise program upload failed");
+    }
+    p->pw.prog = p->pwprog;
+  }
   if (hipMalloc(&p->active, 256) != hipSuccess ||
       hipHostMalloc(&p->active_h, 256, hipHostMallocDefault) != hipSuccess) {
     bsgp_plan_destroy(p);
@@ -392,6 +497,7 @@ int bsgp_plan_destroy(bsgp_plan p) {
   if (p->tpart) (void)hipFree(p->tpart);
   if (p->tctr) (void)hipFree(p->tctr);
   if (p->plist) (void)hipFree(p->plist);
+  if (p->pwprog) (void)hipFree(p->pwprog);
   delete p;
   return BSGP_OK;
 }
@@ -483,6 +589,8 @@ static int check_params(const bsgp_params* q) {
   if (q->init_recon < 0 || q->init_recon > 3) return fail(BSGP_ERR_ARG, "bad init_recon");
   if (q->proj_type != 0 && q->proj_type != 1) return fail(BSGP_ERR_ARG, "bad proj_type");
   if (q->scale_data < 0 || q->scale_data > 2) return fail(BSGP_ERR_ARG, "bad scale_data");
+  if (q->gn_f32 && q->scale_data != 2)
+    return fail(BSGP_ERR_ARG, "gn_f32 needs scale_data == 2 (the caller scales in float32)");
   return BSGP_OK;
 }
 
@@ -496,6 +604,7 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   if ((prm->init_recon == 1 || prm->scale_data == 2) && !in->x0)
     return fail(BSGP_ERR_ARG, "init_recon=1 and scale_data=2 need x0");
   if (!out || !out->x || !out->iters || !out->discr) return fail(BSGP_ERR_ARG, "outputs missing");
+  if (out->err && !in->obj) return fail(BSGP_ERR_ARG, "err needs the ground truth obj");
   if (p->n_tf > 1 && B != p->n_tf)
     return fail(BSGP_ERR_ARG, "the plan holds one PSF per image: B must equal its PSF count");
   HIP_TRY(hipSetDevice(p->device));
@@ -534,6 +643,7 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   a.plist = nullptr;
   a.plist_stride = 0;
   a.lcap = 0;
+  a.pw = p->pw;
   if (prm->proj_cache && prm->proj_type == 1) {
     a.lcap = proj_list_cap(p->g, T);
     const size_t half = round_up((size_t)a.lcap * T * kBlock, 32);
@@ -567,6 +677,9 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   HIP_TRY(hipMemsetAsync(p->tctr, 0, p->tctr_bytes, s));
   hipStream_t ss[bsgp_plan_s::kMaxStreams];
   SolveArgs sa[bsgp_plan_s::kMaxStreams];
+  // per-iteration error / iterate snapshots (errflag, save): one small kernel
+  // after setup and after every iteration, off the hot kernels
+  const bool track = out->err != nullptr || out->x_iter != nullptr;
   if (S > 1) HIP_TRY(hipEventRecord(p->ev_fork, s));
   for (int j = 0; j < S; ++j) {
     ss[j] = S > 1 ? p->sub[j] : s;
@@ -575,13 +688,17 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     sa[j].img0 = (int)((int64_t)B * j / S);
     sa[j].nimg = (int)((int64_t)B * (j + 1) / S) - sa[j].img0;
     HIP_TRY(launch_setup(sa[j], p->lds_bytes, ss[j]));
+    if (track) HIP_TRY(launch_track(sa[j], 0, ss[j]));
   }
   // Fixed-length runs (stop_criterion 0/1) are launched back to back with no
   // host synchronisation; data-dependent stop rules poll the counter.
   const bool data_stop = prm->stop_criterion >= 2 && prm->stop_criterion <= 4;
   const int poll = data_stop ? (B <= 4 ? 1 : 4) : 0;
   for (int it = 1; it <= prm->MAXIT; ++it) {
-    for (int j = 0; j < S; ++j) HIP_TRY(launch_iteration(sa[j], K, p->lds_bytes, ss[j]));
+    for (int j = 0; j < S; ++j) {
+      HIP_TRY(launch_iteration(sa[j], K, p->lds_bytes, ss[j]));
+      if (track) HIP_TRY(launch_track(sa[j], it, ss[j]));
+    }
     if (poll && it < prm->MAXIT && it % poll == 0) {
       for (int j = 0; j < S; ++j) HIP_TRY(hipStreamSynchronize(ss[j]));
       HIP_TRY(hipMemcpyAsync(p->active_h, p->active, sizeof(int), hipMemcpyDeviceToHost, ss[0]));
@@ -625,6 +742,7 @@ int bsgp_solve_host(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_i
   if (in->flux) di.flux = (const double*)dalloc(B * 8);
   if (in->x0) di.x0 = (const double*)dalloc(B * N * 8);
   if (in->beta0) di.beta0 = (const double*)dalloc(B * 8);
+  if (in->obj) di.obj = (const double*)dalloc(B * N * 8);
   dout.x = (double*)dalloc(B * N * 8);
   dout.iters = (int32_t*)dalloc(B * 4);
   dout.discr = (double*)dalloc(B * M1 * 8);
@@ -633,6 +751,8 @@ int bsgp_solve_host(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_i
   if (out->flags) dout.flags = (int32_t*)dalloc(B * M1 * 4);
   if (out->beta_final) dout.beta_final = (double*)dalloc(B * 8);
   if (out->counters) dout.counters = (int64_t*)dalloc(B * 8 * 8);
+  if (out->err) dout.err = (double*)dalloc(B * M1 * 8);
+  if (out->x_iter) dout.x_iter = (double*)dalloc(B * (M1 - 1) * N * 8);
   for (void* b : bufs)
     if (!b) {
       cleanup();
@@ -644,7 +764,8 @@ int bsgp_solve_host(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_i
   bool ok = h2d(di.gn, in->gn, B * N * 8) && h2d(di.bkg, in->bkg, nb * 8) &&
             (!in->flux || h2d(di.flux, in->flux, B * 8)) &&
             (!in->x0 || h2d(di.x0, in->x0, B * N * 8)) &&
-            (!in->beta0 || h2d(di.beta0, in->beta0, B * 8));
+            (!in->beta0 || h2d(di.beta0, in->beta0, B * 8)) &&
+            (!in->obj || h2d(di.obj, in->obj, B * N * 8));
   if (!ok) {
     cleanup();
     return fail(BSGP_ERR_HIP, "host to device copy failed");
@@ -664,7 +785,9 @@ int bsgp_solve_host(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_i
        (!out->crit || d2h(out->crit, dout.crit, B * M1 * 8)) &&
        (!out->flags || d2h(out->flags, dout.flags, B * M1 * 4)) &&
        (!out->beta_final || d2h(out->beta_final, dout.beta_final, B * 8)) &&
-       (!out->counters || d2h(out->counters, dout.counters, B * 64));
+       (!out->counters || d2h(out->counters, dout.counters, B * 64)) &&
+       (!out->err || d2h(out->err, dout.err, B * M1 * 8)) &&
+       (!out->x_iter || d2h(out->x_iter, dout.x_iter, B * (M1 - 1) * N * 8));
   cleanup();
   if (!ok) return fail(BSGP_ERR_HIP, "solve or device to host copy failed");
   return BSGP_OK;

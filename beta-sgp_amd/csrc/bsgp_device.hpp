@@ -1101,6 +1101,10 @@ struct Objective {
   double beta;
   double scal, c1, c2;  // s, s*(b-1), s*b
   int mode;             // 0 KL, 1 beta=0, 2 beta=1, 3 general
+  // float32 observed image (params.gn_f32): numpy 1.x evaluates (s*b)*gn as
+  // float32(s*b) * gn in float32 before the float64 multiply (sgp.py:458)
+  bool f32g;
+  float c2f;
   __device__ __forceinline__ void set_beta(double b) {
     beta = b;
     if (variant == 0) {
@@ -1114,7 +1118,12 @@ struct Objective {
       scal = 1 / (b * (b - 1));
       c1 = scal * (b - 1);
       c2 = scal * b;
+      c2f = (float)c2;
     }
+  }
+  // the gn factor of the third sum: (s*b)*gn, or its float32 rounding
+  __device__ __forceinline__ double c2g(double gnv) const {
+    return f32g ? (double)(c2f * (float)gnv) : c2 * gnv;
   }
   // constant-in-lambda part for one pixel (mode 2: gn; mode 3: s*gn^b)
   __device__ __forceinline__ double konst(double gnv) const {
@@ -1134,6 +1143,10 @@ struct Objective {
       const double p = fpow(den, beta - 1);
       t[0] += c1 * (den * p);
       t[1] += (c2 * gnv) * p;
+    } else if constexpr (MODE == 4) {  // general beta, float32 observed image
+      const double p = fpow(den, beta - 1);
+      t[0] += c1 * (den * p);
+      t[1] += (double)(c2f * (float)gnv) * p;
     } else {
       terms(xtf_try, den, gnv, t);
     }
@@ -1153,7 +1166,7 @@ struct Objective {
     } else {
       const double p = fpow(den, beta - 1);
       t[0] += c1 * (den * p);
-      t[1] += (c2 * gnv) * p;
+      t[1] += c2g(gnv) * p;
     }
   }
   // f from the constant sum K and the two lambda sums

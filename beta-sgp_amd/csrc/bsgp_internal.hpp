@@ -38,6 +38,14 @@ struct ImgState {
 #define BSGP_FUSE_COL 2
 #endif
 
+// numpy float32 reduction program of a plan's N (bsgp_api.hip pairwise_program):
+// [nleaf][2] leaves (start, len), [nnode][2] node operands (value indices),
+// [nlev + 1] level offsets into the nodes, [nchunk] root value of each chunk.
+struct PwProg {
+  const int* prog;
+  int nleaf, nnode, nlev, nchunk;
+};
+
 struct SolveArgs {
   Geo g;
   bsgp_params prm;
@@ -63,10 +71,12 @@ struct SolveArgs {
   double* plist;
   size_t plist_stride;  // doubles per image (both arrays)
   int lcap;             // list capacity per thread (pixels one thread streams)
+  PwProg pw;            // numpy float32 sum order over N (params.gn_f32)
 };
 
 hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s);
 hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s);
+hipError_t launch_track(const SolveArgs& a, int it, hipStream_t s);
 hipError_t launch_build_tf(const Geo& g, const double* kc, cd* spec, cd* tf, double scale,
                            int conj, size_t lds, hipStream_t s);
 hipError_t launch_build_tfs(const Geo& g, int n, const double* kc, size_t kc_stride, cd* spec,

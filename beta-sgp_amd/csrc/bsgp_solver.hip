@@ -230,12 +230,20 @@ __device__ __forceinline__ Dir make_dir(const SolveArgs& A, const ImgState& st) 
   D.hi = st.hi;
   D.lam_p = st.lam_p;
   D.clip = ProjClip{A.prm.has_sat != 0, A.prm.ccd_sat_level / st.sc - 2.220446049250313e-16};
+  // float32 image, proj_type 0: the first scaling matrix is x.copy() of the
+  // float32 start, clipped (compared and assigned) at float32 bounds
+  // (sgp.py:279-285 / 723-729); from iteration 2 on x is float64
+  if (A.prm.gn_f32 && A.prm.proj_type == 0 && st.iter == 1) {
+    D.lo = (double)(float)st.lo;
+    D.hi = (double)(float)st.hi;
+  }
   return D;
 }
 
 __device__ __forceinline__ Objective make_obj(const SolveArgs& A, double beta) {
   Objective o;
   o.variant = A.prm.variant;
+  o.f32g = A.prm.gn_f32 != 0;
   o.set_beta(beta);
   return o;
 }
@@ -268,6 +276,48 @@ __device__ __forceinline__ bool leader(const Team& t) { return t.m == 0 && threa
   extern __shared__ __attribute__((aligned(16))) char smem[];                      \
   cd* lds = reinterpret_cast<cd*>(smem);                                           \
   double* red = reinterpret_cast<double*>(smem + (A).lds_fft_bytes)
+
+// numpy's float32 np.sum of term(i) for i < N, in numpy's exact order (the
+// plan's PwProg, bsgp_api.hip pairwise_program): the leaves by the team's
+// threads (each a numpy leaf: 8 strided float32 accumulators), the inner nodes
+// level by level with a team barrier between levels, then the chunk fold
+// res = res + root from 0.  `vals` is float scratch in HBM (leaves + nodes).
+template <class TERM>
+__device__ float np_f32_sum(const PwProg& pw, TERM&& term, float* vals, const Part& D, Team& tm) {
+  const int* lv = pw.prog;
+  const int* nd = lv + 2 * pw.nleaf;
+  const int* off = nd + 2 * pw.nnode;
+  const int* roots = off + pw.nlev + 1;
+  for (int l = D.gt0 + (int)threadIdx.x; l < pw.nleaf; l += D.gts) {
+    const int s0 = lv[2 * l], n = lv[2 * l + 1];
+    float res;
+    if (n < 8) {
+      res = 0.0f;
+      for (int i = 0; i < n; ++i) res += term(s0 + i);
+    } else {
+      float r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = term(s0 + j);
+      int i = 8;
+      for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += term(s0 + i + j);
+      }
+      res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+      for (; i < n; ++i) res += term(s0 + i);
+    }
+    vals[l] = res;
+  }
+  team_sync(tm);
+  for (int h = 0; h < pw.nlev; ++h) {
+    for (int k = off[h] + D.gt0 + (int)threadIdx.x; k < off[h + 1]; k += D.gts)
+      vals[pw.nleaf + k] = vals[nd[2 * k]] + vals[nd[2 * k + 1]];
+    team_sync(tm);
+  }
+  float res = 0.0f;
+  for (int c = 0; c < pw.nchunk; ++c) res = res + vals[roots[c]];
+  return res;
+}
 
 // ------------------------------------------------------------ kernel: setup
 // sgp.py:163-298 (= 617-742): scaling, null pixels, flux, x0, initial
@@ -355,7 +405,9 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     B.xa[N] = B.xb[N] = B.ga[N] = B.gb[N] = B.xtf[N] = B.dtf[N] = 0.0;
   }
   team_sum<1>(v1, red, tm);
-  const double flux = A.in.flux ? A.in.flux[img] / sc : v1[0];  // sgp.py:208-211
+  // sgp.py:208-211 (scale_data 2: the caller scaled the flux in its own dtype)
+  const double flux =
+      A.in.flux ? (P.scale_data == 2 ? A.in.flux[img] : A.in.flux[img] / sc) : v1[0];
   const ProjClip clip{P.has_sat != 0, P.ccd_sat_level / sc - eps};
 
   // initial projection with dia = 1 (sgp.py:250-253); every thread clips the
@@ -374,6 +426,18 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   // x_tf = A(x), f and g (sgp.py:260-265 / 702-709)
   const double beta0 = A.in.beta0 ? A.in.beta0[img] : P.betaParam;
   Objective obj = make_obj(A, beta0);
+  // float32 image: the lambda-independent sum np.sum(s*gn**beta) is a float32
+  // array reduced by numpy in float32 (sgp.py:458); its order is the plan's
+  // pairwise program.  The dtf vector is free scratch until the first k_ls.
+  const bool konst_f32 = P.gn_f32 && P.variant == BSGP_VARIANT_BETA && obj.mode == 3;
+  double konst32 = 0.0;
+  if (konst_f32) {
+    const float sf = (float)obj.scal;
+    const double bf = (double)(float)obj.beta;  // x**beta: the exponent is cast to float32
+    konst32 = (double)np_f32_sum(
+        A.pw, [&](int i) { return sf * (float)pow(B.gns[i], bf); },
+        reinterpret_cast<float*>(B.dtf), D, tm);
+  }
   double fsum[3] = {0.0, 0.0, 0.0};  // K, T0, T1
   row_fwd<COOP>(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.xa[r * G.W + j]; });
   team_sync(tm);
@@ -394,6 +458,7 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   });
   team_sum<3>(fsum, red, tm);
   team_sync(tm);  // publishes xtf / spec / pw
+  if (konst_f32) fsum[0] = konst32;
   const double fv = obj.combine(fsum[0], fsum[1], fsum[2], flux, (double)N);
   col_conv<COOP>(G, D, B.spec, tf_of(G, img, 1), lds);
   team_sync(tm);
@@ -838,6 +903,11 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   };
   double fr = st.Fold[0];
   for (int k = 1; k < P.M; ++k) fr = py_max2(fr, st.Fold[k]);
+  // lam = beta^(k-1) at trial k; lam < 1e-12 forces acceptance (sgp.py:336),
+  // so for 0 < beta < 1 the cap below is never reached
+  const int ls_cap = (P.beta > 0.0 && P.beta < 1.0)
+                         ? (int)ceil(log(1e-12) / log(P.beta)) + 2
+                         : 4096;
   Objective obj = make_obj(A, st.beta);
   double lam = 1.0;
   double f_acc = 0.0;
@@ -855,7 +925,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   // over the image (truncation < 1e-17 relative at MS = 6: (0.01)^7 * binom).
   constexpr int MS = 6;
   constexpr double kSeriesRho = 0.01;
-  const bool series = MODE == 3 && !adapt && P.ls_series != 0;
+  const bool series = (MODE == 3 || MODE == 4) && !adapt && P.ls_series != 0;
   double Pm[MS + 1], Qm[MS + 1];
   double rho = INFINITY;
   // ---- pass 1, fused into the inverse rows that produce d_tf: lam = 1 direct
@@ -895,7 +965,8 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
         const double a = x0 + bkv;
         const double u = v / a;
         const double p0 = q.p0;  // = fpow(a, beta-1), stored at the last accept
-        const double A0 = a * p0, B0 = g * p0;
+        // MODE 4: the float32-rounded (s*b)*gn factor; combined without c2 below
+        const double A0 = a * p0, B0 = (MODE == 4 ? (double)(obj.c2f * (float)g) : g) * p0;
         double um = 1.0;
 #pragma unroll
         for (int m = 0; m <= MS; ++m) {
@@ -952,7 +1023,8 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
         s1 += cb1[m] * lm * Qm[m];
         lm *= lam;
       }
-      const double fk = obj.combine(konst, obj.c1 * s0, obj.c2 * s1, flux, (double)N);
+      const double fk =
+          obj.combine(konst, obj.c1 * s0, (MODE == 4 ? 1.0 : obj.c2) * s1, flux, (double)N);
       ++nls;
       ++series_evals;
       if (fk <= fr + P.gamma * lam * gd || lam < 1e-12) {
@@ -961,7 +1033,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
         break;
       }
       lam = lam * P.beta;
-      if (nls > 64) {
+      if (nls > ls_cap) {
         status = 1;
         break;
       }
@@ -1038,7 +1110,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
       const double bgrad = (obj.beta == 0.0 || obj.beta == 1.0) ? 0.0 : t[2 * K + 1] / N;
       obj.set_beta(obj.beta - lr_st * bgrad);
     }
-    if (nls > 64) {  // unreachable: lam < 1e-12 forces acceptance by the 32nd trial
+    if (nls > ls_cap) {  // only for beta outside (0, 1): the reference never terminates
       status = 1;
       break;
     }
@@ -1245,6 +1317,40 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
       }
       atomicSub(A.active, 1);
     }
+  }
+}
+
+// ---------------------------------------- kernel: per-iteration tracking
+// errflag / save (sgp.py:240-257, 394-396, 416-422): launched after setup
+// (it = 0) and after iteration it; for every image whose iteration `it` ran it
+// writes the relative error of the scaled iterate against obj/scaling and a
+// copy of the iterate (after the update, before any revert).  Off the hot
+// kernels: only solves that ask for err / x_iter launch it.
+__global__ void __launch_bounds__(kBlock) k_track(SolveArgs A, int it) {
+  __shared__ double red[(kWaves + 1) * kMaxRed];
+  const int img = A.img0 + (int)blockIdx.x;
+  const ImgState& st = A.st[img];
+  if (it > 0 && st.iter != it + 1) return;  // iteration `it` did not run for this image
+  const int N = A.g.H * A.g.W;
+  const Bufs B = slot_bufs(A, img, st.par);
+  // k_bb flips `par` when the image goes on; a stopping image keeps it
+  const double* x = (it == 0 || !st.stop) ? B.xa : B.xb;
+  const int tid = threadIdx.x;
+  if (A.out.err) {
+    const double* o = A.in.obj + (size_t)img * N;
+    double s[2] = {0.0, 0.0};
+    for (int i = tid; i < N; i += kBlock) {
+      const double ov = o[i] / st.sc;  // obj / scaling (sgp.py:243)
+      const double e = x[i] - ov;
+      s[0] += e * e;
+      s[1] += ov * ov;
+    }
+    block_sum<2>(s, red);
+    if (tid == 0) A.out.err[(size_t)img * (A.prm.MAXIT + 1) + it] = sqrt(s[0] / s[1]);
+  }
+  if (A.out.x_iter && it > 0) {
+    double* d = A.out.x_iter + ((size_t)img * A.prm.MAXIT + (it - 1)) * N;
+    for (int i = tid; i < N; i += kBlock) d[i] = x[i];
   }
 }
 
@@ -1489,10 +1595,10 @@ static void launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipStream_
   // line-search kernel specialised on trial width, objective mode, adaptivity
   const bsgp_params& P = a.prm;
   const bool adapt = P.adapt_beta && P.variant == BSGP_VARIANT_BETA;
-  const int mode = P.variant == BSGP_VARIANT_KL ? 0
-                   : (P.betaParam == 0.0 || P.betaParam == 1.0 || a.in.beta0) ? -1
-                                                                                : 3;
+  const bool special = a.in.beta0 ? !P.beta0_general : (P.betaParam == 0.0 || P.betaParam == 1.0);
+  const int mode = P.variant == BSGP_VARIANT_KL ? 0 : special ? -1 : P.gn_f32 ? 4 : 3;
   if (COOP && K > 2) K = 2;  // cooperative builds carry trial widths 1 and 2
+  if (mode == 4 && K > 2) K = 2;
   if (adapt) {
     hipLaunchKernelGGL((k_ls<1, -1, true, COOP>), grid, block, lds, s, a);
   } else if (mode == 0) {
@@ -1509,6 +1615,11 @@ static void launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipStream_
       case 4: hipLaunchKernelGGL((k_ls<4, 3, false, false>), grid, block, lds, s, a); break;
       default: hipLaunchKernelGGL((k_ls<8, 3, false, false>), grid, block, lds, s, a); break;
     }
+  } else if (mode == 4) {
+    if (K == 1)
+      hipLaunchKernelGGL((k_ls<1, 4, false, COOP>), grid, block, lds, s, a);
+    else
+      hipLaunchKernelGGL((k_ls<2, 4, false, COOP>), grid, block, lds, s, a);
   } else {
     hipLaunchKernelGGL((k_ls<2, -1, false, COOP>), grid, block, lds, s, a);
   }
@@ -1520,6 +1631,10 @@ hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s
     launch_iteration_t<true>(a, K, lds, s);
   else
     launch_iteration_t<false>(a, K, lds, s);
+  return hipGetLastError();
+}
+hipError_t launch_track(const SolveArgs& a, int it, hipStream_t s) {
+  hipLaunchKernelGGL(k_track, dim3(a.nimg), dim3(kBlock), 0, s, a, it);
   return hipGetLastError();
 }
 hipError_t launch_build_tf(const Geo& g, const double* kc, cd* spec, cd* tf, double scale,
@@ -1628,6 +1743,10 @@ hipError_t set_solver_lds_limit(size_t bytes) {
                        (const void*)k_ls<4, 3, false, false>,
                        (const void*)k_ls<8, 3, false, false>,
                        (const void*)k_ls<2, -1, false, false>,
+                       (const void*)k_ls<1, 4, false, false>,
+                       (const void*)k_ls<2, 4, false, false>,
+                       (const void*)k_ls<1, 4, false, true>,
+                       (const void*)k_ls<2, 4, false, true>,
                        (const void*)k_bb<false>,
                        (const void*)apply_op_kernel<false>,
                        (const void*)k_setup<true>,

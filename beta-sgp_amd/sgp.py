@@ -21,19 +21,30 @@ lines (sgp.py:104, 291-298, 351-352, 399-411), the final prints of
 revert-to-previous-iterate on stop (sgp.py:424-425) and the returned tuple
 ``(x, iters, discr, times, None)``.
 
-Deliberate differences: ``save=True`` (per-iteration FITS
-dumps) and ``errflag=True`` raise ``NotImplementedError``; a plain Python
-float ``bkg`` is accepted (the reference crashes on ``bkg.flatten()``).
+``save=True`` writes the reference's per-iteration FITS files
+(SGP_reconstructed_images/, sgp.py:223-231, 416-422) from device snapshots of
+every iterate; ``errflag=True`` (``sgp`` only, as in the reference) returns
+the per-iteration error as the fifth element (sgp.py:240-257, 394-396).
+A float32 image is scaled in float32 on the host and solved with the
+reference's float32 arithmetic reproduced on the device (numpy 1.x rules;
+include/bsgp.h ``gn_f32``).
+
+Deliberate differences: a plain Python float ``bkg`` is
+accepted (the reference crashes on ``bkg.flatten()``); errflag at MAXIT
+returns the error array instead of the reference's IndexError.
 
 Extra: :func:`sgp_betaDiv_batch` / :func:`sgp_batch` solve
 many images or beta candidates in one launch.
 """
+import errno
 import logging
 import math
+import os
 
 import numpy as np
 
 import _bsgp as _B
+import fits_io
 
 DEFAULT_PARAMS = (1000, 1e-4, 0.4, 1e-5, 1e5, 1e1, 3, 0.5, 1)  # sgp.py:34
 DEFAULT_COLUMNS = ['label', 'xcentroid', 'ycentroid', 'sky_centroid',
@@ -69,9 +80,34 @@ def _bkg_kind(bkg, shape):
     raise ValueError(f"bkg of shape {b.shape} does not broadcast to the image shape {shape}")
 
 
+def _scalar_dtype(v):
+    if isinstance(v, (np.generic, np.ndarray)):
+        return np.asarray(v).dtype
+    return np.dtype(np.float64) if isinstance(v, float) else np.dtype(np.int64)
+
+
+def _np1_scalar_div(a, b):
+    """a / b of two scalars as numpy 1.x computes it (the reference's numpy:
+    the golden fixtures come from numpy 1.26): scalar-with-scalar operations
+    promote by type, a Python float counting as float64, so float32 / float32
+    stays float32 and a Python float over a float32 scaling is float64."""
+    rt = np.promote_types(_scalar_dtype(a), _scalar_dtype(b))
+    if rt.kind != "f":
+        rt = np.dtype(np.float64)
+    return rt.type(np.asarray(a, dtype=rt) / np.asarray(b, dtype=rt))
+
+
 def _prelude_host(gn, bkg, init_recon, flux, stop_criterion, scale_data):
-    """sgp.py:166-199 in the input dtype (used for non-float64 images so the
-    scaling rounds exactly like the reference's numpy code)."""
+    """sgp.py:166-211 (= 619-666) for a float32 image, in float32 with numpy
+    1.x promotion: an array never widens for a Python or 0-d operand, scalars
+    promote by type.  Returns the scaled, null-pixel-fixed float32 image, the
+    scaled background (its own dtype), the scaled start x, the scaling, the
+    stop-rule-4 tolerance and the scaled flux (None: the device sums it)."""
+    gn = np.asarray(gn)
+    gn = gn.astype(gn.dtype.newbyteorder("="), copy=True)  # native order, same values
+    dt = gn.dtype
+    bk = np.asarray(bkg)
+    bk = bk.astype(bk.dtype.newbyteorder("="))
     if init_recon == 0:
         x = np.zeros_like(gn)
     elif init_recon == 1:
@@ -81,28 +117,48 @@ def _prelude_host(gn, bkg, init_recon, flux, stop_criterion, scale_data):
         x = gn.copy()
     else:
         if flux is None:
-            x = np.sum(gn - bkg) / gn.size * np.ones_like(gn)
+            v = _np1_scalar_div(np.sum(gn - (bk.astype(dt) if bk.ndim == 0 else bk)), gn.size)
         else:
-            x = flux / gn.size * np.ones_like(gn)
+            v = _np1_scalar_div(flux, gn.size)
+        x = np.full(gn.shape, v).astype(dt)  # v * ones_like(gn) runs in gn's dtype
     gn = gn.flatten()
     x = x.flatten()
-    bkg = np.asarray(bkg).flatten()
-    tol4 = 1 + 1 / np.mean(gn) if stop_criterion == 4 else 0.0
+    bkf = bk.flatten()
+    tol4 = 1 + 1 / float(np.mean(gn)) if stop_criterion == 4 else 0.0
     if scale_data:
         scaling = np.max(gn)
         gn = gn / scaling
-        bkg = bkg / scaling
+        bkf = bkf / scaling
         x = x / scaling
     else:
         scaling = 1.
-    return gn, bkg, x, float(scaling), float(tol4)
+    vmin = np.min(gn[gn > 0])
+    gn[gn <= 0] = np.float64(vmin) * np.finfo(float).eps * np.finfo(float).eps
+    if flux is not None:
+        flux_s = _np1_scalar_div(flux, scaling)
+    elif bkf.dtype != np.float64:
+        flux_s = np.sum(gn - bkf)  # float32 background: numpy's float32 reduction (sgp.py:209)
+    else:
+        flux_s = None  # float64 sum, on the device
+    return gn, bkf, x, float(scaling), float(tol4), flux_s
+
+
+def _gn_scaled_host(gn, scale_data):
+    """The scaled, null-pixel-fixed float64 image of sgp.py:193-204, for the
+    FITS files of save=True only (orig.fits, res_k.fits)."""
+    g = np.asarray(gn, dtype=np.float64).flatten()
+    if scale_data:
+        g = g / np.max(g)
+    vmin = np.min(g[g > 0])
+    g[g <= 0] = vmin * np.finfo(float).eps * np.finfo(float).eps
+    return g
 
 
 def _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, alpha, alpha_min,
             alpha_max, M_alpha, tau, M, max_projs, verbose, ccd_sat_level, scale_data,
             tol_convergence, adapt_beta=False, betaParam=1.005, lr=1e-3, lr_exp_param=0.1,
             schedule_lr=False, bkg_is_map=False, ls_spec=None, ls_series=None, streams=None,
-            team=None, proj_cache=None, gn_compact=None):
+            team=None, proj_cache=None, gn_compact=None, betaParams=None):
     p = _B.Params()
     p.variant = variant
     p.init_recon = int(init_recon)
@@ -130,6 +186,10 @@ def _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, 
     p.team = TEAM_DEFAULT if team is None else int(team)
     p.proj_cache = PROJ_CACHE_DEFAULT if proj_cache is None else int(bool(proj_cache))
     p.gn_compact = GN_COMPACT_DEFAULT if gn_compact is None else int(bool(gn_compact))
+    p.gn_f32 = 0
+    if betaParams is not None:
+        b0 = np.asarray(betaParams, dtype=np.float64)
+        p.beta0_general = int(bool(np.all((b0 != 0.0) & (b0 != 1.0))))
     return p
 
 
@@ -157,20 +217,59 @@ def _write_log(stop_criterion, verbose, discr, crit, flags, MAXIT, tol):
             log.info(f'it {k} D_k {discr[k]} tol {tol}\n')
 
 
+SAVE_DIR = "SGP_reconstructed_images/"
+
+
+def _save_setup(gs, shape):
+    """sgp.py:223-231 / 678-686: the directory, and orig.fits when it is new."""
+    try:
+        os.mkdir(SAVE_DIR)
+        fits_io.write_fits(f"{SAVE_DIR}/orig.fits", gs.reshape(shape))
+    except OSError as exc:
+        if exc.errno != errno.EEXIST:
+            raise OSError("Directory already exists!")
+
+
+def _save_iterates(x_iter, gs, shape):
+    """sgp.py:416-422 / 870-876: rec_k.fits (the scaled iterate after iteration
+    k, before the revert) and res_k.fits = (x - gn) / sqrt(x)."""
+    for k in range(x_iter.shape[0]):
+        x = x_iter[k].reshape(-1)
+        fits_io.write_fits(f"SGP_reconstructed_images/rec_{k + 1}.fits", x.reshape(shape),
+                           overwrite=True)
+        with np.errstate(all="ignore"):
+            res = np.divide(x - gs, np.sqrt(x))
+        fits_io.write_fits(f"SGP_reconstructed_images/res_{k + 1}.fits", res.reshape(shape),
+                           overwrite=True)
+
+
+def _err_layout(e, it):
+    """The reference's err array (sgp.py:241, 257, 394-396, 431-432): err[0]
+    after the initial projection, then the error after iteration k stored at
+    index k+1 (the increment comes first), cut to iters+1 entries, so err[1]
+    stays 0 and the last iteration's error is dropped.  At MAXIT the
+    reference's store overruns its array (IndexError); this returns what the
+    array would have held."""
+    err = np.zeros(it + 1)
+    err[0] = e[0]
+    if it >= 2:
+        err[2:] = e[1:it]
+    return err
+
+
 def _run(variant, gn, psf, bkg, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta,
          alpha, alpha_min, alpha_max, M_alpha, tau, M, max_projs, save, obj, verbose, flux,
          ccd_sat_level, scale_data, errflag, tol_convergence, use_original_SGP_Afunction,
-         beta_kw):
+         beta_kw, betas=None):
+    """One drop-in solve; with ``betas`` (beta variant) the same image is solved
+    for every initial betaParam in one batched launch and a list of results is
+    returned (the multi-start of application_sgp_subdivisions.py:83-99)."""
     _check_psf(psf)
     logging.basicConfig(filename='sgp.log', level=logging.INFO, force=True)
+    # sgp_betaDiv has no error path: errflag / obj are accepted and ignored
+    errflag = bool(errflag) and variant == _B.BSGP_VARIANT_KL
     if errflag and obj is None:
         raise ValueError("errflag was set to True but no ground-truth was passed.")
-    if save:
-        raise NotImplementedError("save=True (per-iteration FITS dumps) is not supported by the "
-                                  "device engine")
-    if errflag:
-        raise NotImplementedError("errflag=True (per-iteration error vs obj) is not supported by "
-                                  "the device engine")
     gn = np.asarray(gn)
     psf = np.asarray(psf)
     _shape = gn.shape
@@ -187,30 +286,61 @@ def _run(variant, gn, psf, bkg, init_recon, proj_type, stop_criterion, MAXIT, ga
     bkg_is_map = kind == "map"
     prm = _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, alpha,
                   alpha_min, alpha_max, M_alpha, tau, M, max_projs, verbose, ccd_sat_level,
-                  scale_data, tol_convergence, bkg_is_map=bkg_is_map, **beta_kw)
+                  scale_data, tol_convergence, bkg_is_map=bkg_is_map, betaParams=betas,
+                  **beta_kw)
     x0 = None
-    native_f64 = gn.dtype == np.float64
-    if native_f64:
-        g = gn
+    fl = None if flux is None else np.array([float(flux)])
+    f32 = gn.dtype.kind == "f" and gn.dtype.itemsize == 4
+    if f32:
+        # the reference computes in the image's float32 (sgp.py:193-211): scale
+        # on the host in float32, and let the device reproduce the float32
+        # parts of the beta objective (include/bsgp.h gn_f32)
+        g, bk, x0, scaling, tol4, flux_s = _prelude_host(
+            gn, b if bkg_is_map else np.asarray(bkg).reshape(()), init_recon, flux,
+            stop_criterion, scale_data)
+        prm.scale_data = 2
+        prm.prescaled_scaling = scaling
+        prm.prescaled_tol4 = tol4
+        prm.gn_f32 = 1
+        fl = None if flux_s is None else np.array([float(flux_s)])
+    else:
+        # float64 in any byte order (and integer images, which numpy's
+        # true division turns into float64 at the scaling, sgp.py:195)
+        g = np.asarray(gn, dtype=np.float64)
         bk = b
         if init_recon == 1:
             np.random.seed(42)
             x0 = np.random.randn(*gn.shape)
-    else:
-        # reference scaling in the input dtype (sgp.py:193-197), done on the host
-        g, bk, x0, scaling, tol4 = _prelude_host(gn, b if bkg_is_map else b.reshape(()),
-                                                 init_recon, flux, stop_criterion, scale_data)
-        prm.scale_data = 2
-        prm.prescaled_scaling = scaling
-        prm.prescaled_tol4 = tol4
     plan = _B.get_plan(_shape[0], _shape[1], psf, mode)
     gd = _B.to_dev(np.asarray(g, dtype=np.float64).reshape(1, *_shape))
     bd = _B.to_dev(np.asarray(bk, dtype=np.float64).reshape((1, *_shape) if bkg_is_map else (1,)))
-    fd = None if flux is None else _B.to_dev(np.array([float(flux)]))
+    fd = None if fl is None else _B.to_dev(fl)
     xd = None if x0 is None else _B.to_dev(np.asarray(x0, dtype=np.float64).reshape(1, *_shape))
-    out = plan.solve(gd, bd, prm, flux=fd, x0=xd)
+    od = None if not errflag else _B.to_dev(np.asarray(obj, dtype=np.float64).reshape(1, *_shape))
+    gs = None
+    if save:
+        gs = np.asarray(g, dtype=np.float64).reshape(-1) if f32 else _gn_scaled_host(g, scale_data)
+        _save_setup(np.asarray(g).reshape(-1) if f32 else gs, _shape)
+    b0 = None
+    if betas is not None:
+        nb = len(betas)
+        gd, bd, xd, od = (None if t is None else t.expand(nb, *t.shape[1:]).contiguous()
+                          for t in (gd, bd, xd, od))
+        fd = None if fd is None else fd.expand(nb).contiguous()
+        b0 = _B.to_dev(np.asarray(betas, dtype=np.float64))
+    out = plan.solve(gd, bd, prm, flux=fd, x0=xd, obj=od, beta0=b0, want_iterates=bool(save))
     _B.torch.cuda.current_stream().synchronize()
     _B.check_status(out["counters"])
+    if betas is not None:
+        res = []
+        for i in range(len(betas)):
+            it = int(out["iters"][i])
+            res.append((out["x"][i].cpu().numpy().reshape(_shape), it,
+                        out["discr"][i, :it + 1].cpu().numpy(),
+                        out["times"][i, :it + 1].cpu().numpy(),
+                        {"beta": float(out["beta_final"][i]),
+                         "counters": out["counters"][i].cpu().numpy(), "err": None}))
+        return res
     it = int(out["iters"][0])
     discr = out["discr"][0, :it + 1].cpu().numpy()
     times = out["times"][0, :it + 1].cpu().numpy()
@@ -222,8 +352,11 @@ def _run(variant, gn, psf, bkg, init_recon, proj_type, stop_criterion, MAXIT, ga
             tol = tol * tol
         _write_log(stop_criterion, verbose, discr, out["crit"][0].cpu().numpy(),
                    out["flags"][0].cpu().numpy(), MAXIT, tol)
+    if save:
+        _save_iterates(out["x_iter"][0, :it].cpu().numpy(), gs, _shape)
     x = out["x"][0].cpu().numpy().reshape(_shape)
-    extra = {"beta": float(out["beta_final"][0]), "counters": out["counters"][0].cpu().numpy()}
+    extra = {"beta": float(out["beta_final"][0]), "counters": out["counters"][0].cpu().numpy(),
+             "err": _err_layout(out["err"][0].cpu().numpy(), it) if errflag else None}
     return x, it, discr, times, extra
 
 
@@ -233,12 +366,12 @@ def sgp(gn, psf, bkg, init_recon=0, proj_type=0, stop_criterion=0, MAXIT=500, ga
         max_projs=1000, save=False, obj=None, verbose=True, flux=None, ccd_sat_level=None,
         scale_data=True, errflag=False, tol_convergence=1e-4, use_original_SGP_Afunction=True):
     """Scaled Gradient Projection with the KL objective (sgp.py:41-438)."""
-    x, it, discr, times, _ = _run(_B.BSGP_VARIANT_KL, gn, psf, bkg, init_recon, proj_type,
-                                  stop_criterion, MAXIT, gamma, beta, alpha, alpha_min,
-                                  alpha_max, M_alpha, tau, M, max_projs, save, obj, verbose,
-                                  flux, ccd_sat_level, scale_data, errflag, tol_convergence,
-                                  use_original_SGP_Afunction, {})
-    return x, it, discr, times, None
+    x, it, discr, times, extra = _run(_B.BSGP_VARIANT_KL, gn, psf, bkg, init_recon, proj_type,
+                                      stop_criterion, MAXIT, gamma, beta, alpha, alpha_min,
+                                      alpha_max, M_alpha, tau, M, max_projs, save, obj, verbose,
+                                      flux, ccd_sat_level, scale_data, errflag, tol_convergence,
+                                      use_original_SGP_Afunction, {})
+    return x, it, discr, times, extra["err"]
 
 
 def sgp_betaDiv(gn, psf, bkg, init_recon=0, proj_type=0, stop_criterion=0, MAXIT=500,
@@ -296,6 +429,24 @@ def lr_schedule(init_lr, k, epoch):
 
 
 # ------------------------------------------------------------------- batched
+def _bkg_batch(bkgs, Bn, H, W):
+    """Backgrounds of a batch as the device expects them: [B] scalars or
+    [B, H, W] maps, float64, contiguous.  Accepted: a scalar, [1] or [B]
+    scalars, one [H, W] (or [1, H, W]) map for every image, or [B, H, W]."""
+    torch = _B.torch
+    t = (bkgs.to(device="cuda", dtype=torch.float64) if torch.is_tensor(bkgs)
+         else _B.to_dev(np.asarray(bkgs, dtype=np.float64)))
+    shape = tuple(t.shape)
+    if t.dim() == 0 or (t.dim() == 1 and shape[0] in (1, Bn)):
+        return t.reshape(-1).expand(Bn).contiguous()
+    if shape in ((H, W), (1, H, W)):
+        return t.reshape(1, H, W).expand(Bn, H, W).contiguous()
+    if shape == (Bn, H, W):
+        return t.contiguous()
+    raise ValueError(f"bkg of shape {shape} fits neither [B]={Bn} scalars nor [B, H, W] maps "
+                     f"of {H}x{W} images")
+
+
 def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon=0, proj_type=0,
                  stop_criterion=0, MAXIT=500, gamma=1e-4, beta=0.4, alpha=1.3, alpha_min=1e-5,
                  alpha_max=1e5, M_alpha=3, tau=0.5, M=1, max_projs=1000, verbose=True,
@@ -309,21 +460,22 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
     if not per_image:
         _check_psf(np.asarray(psf))
     _B.require_gpu()
-    if not torch.is_tensor(gns):
+    if torch.is_tensor(gns):
+        gns = gns.to(device="cuda", dtype=torch.float64).contiguous()
+    else:
         gns = _B.to_dev(np.asarray(gns, dtype=np.float64))
+    if gns.dim() != 3:
+        raise ValueError("gns must be a batch [B, H, W]")
     Bn, H, W = gns.shape
     mode = _B.BSGP_CONV_CIRCULAR if use_original_SGP_Afunction else _B.BSGP_CONV_LINEAR_FILL
-    if not torch.is_tensor(bkgs):
-        bk = np.asarray(bkgs, dtype=np.float64)
-        bk = np.broadcast_to(bk, (Bn,)) if bk.ndim <= 1 and bk.size in (1, Bn) else bk
-        bkgs = _B.to_dev(np.ascontiguousarray(bk))
+    bkgs = _bkg_batch(bkgs, Bn, H, W)
     bkg_is_map = bkgs.dim() == 3
     prm = _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, alpha,
                   alpha_min, alpha_max, M_alpha, tau, M, max_projs, verbose, ccd_sat_level,
                   scale_data, tol_convergence, adapt_beta=adapt_beta, betaParam=betaParam, lr=lr,
                   lr_exp_param=lr_exp_param, schedule_lr=schedule_lr, bkg_is_map=bkg_is_map,
                   ls_spec=ls_spec, ls_series=ls_series, streams=streams,
-                  team=team, proj_cache=proj_cache, gn_compact=gn_compact)
+                  team=team, proj_cache=proj_cache, gn_compact=gn_compact, betaParams=betaParams)
     x0 = None
     if init_recon == 1:
         np.random.seed(42)
@@ -358,3 +510,67 @@ def sgp_betaDiv_batch(gns, psf, bkgs, betaParams=None, **kw):
     multi-start beta search of application_sgp_subdivisions.py:70-107 as one
     launch).  Returns the dict of :func:`sgp_batch` plus beta_final [B]."""
     return _solve_batch(_B.BSGP_VARIANT_BETA, gns, psf, bkgs, betaParams=betaParams, **kw)
+
+
+# --------------------------------------------------------- multi-start beta
+APP_BETA_SEEDS = (0, 42, 951, 93, 810)  # application_sgp_subdivisions.py:71
+
+
+def app_beta_candidates(seeds=APP_BETA_SEEDS, loc=1.0, scale=0.05):
+    """The application's initial betas: one np.random.normal(1, 0.05) draw per
+    seed (application_sgp_subdivisions.py:70-76)."""
+    out = []
+    for s in seeds:
+        np.random.seed(s)
+        out.append(np.random.normal(loc=loc, scale=scale))
+    return out
+
+
+def sgp_betaDiv_multistart(gn, psf, bkg, betas=None, score=None, final_solve=True, **kwargs):
+    """The beta search of application_sgp_subdivisions.py:69-107 as two
+    launches: every candidate initial beta (default: the application's five
+    seeds) is solved in ONE batched launch, the host takes the argmin of
+    ``score(x)`` over the candidates, and -- as the application does -- the
+    image is solved once more with the best initial beta.
+
+    ``score`` is the application's criterion, the photometric flux fractional
+    difference 1 - sum(segment_flux(x)) / sum(segment_flux(gn)) (:92-99); it
+    needs photutils, which this package does not carry, so the caller passes
+    it.  Without one the candidates are ranked by their final discrepancy
+    discr[-1] (a stand-in, not the application's choice).  ``kwargs`` are
+    sgp_betaDiv's keyword arguments.
+
+    Returns (x, iters, discr, times, None) of the final solve and a dict with
+    "betas", "scores", "best_beta" and "candidates" (each candidate's
+    (x, iters, discr, times, None))."""
+    betas = list(app_beta_candidates() if betas is None else betas)
+    kw = dict(kwargs)
+    kw.pop("betaParam", None)
+    bkw = {k: kw.pop(k) for k in ["adapt_beta", "lr", "lr_exp_param", "schedule_lr"] if k in kw}
+    bkw.setdefault("adapt_beta", True)  # sgp_betaDiv's default (sgp.py:510)
+    args = dict(init_recon=0, proj_type=0, stop_criterion=0, MAXIT=500, gamma=1e-4, beta=0.4,
+                alpha=1.3, alpha_min=1e-5, alpha_max=1e5, M_alpha=3, tau=0.5, M=1,
+                max_projs=1000, save=False, obj=None, verbose=True, flux=None,
+                ccd_sat_level=None, scale_data=True, errflag=False, tol_convergence=1e-4,
+                use_original_SGP_Afunction=True)
+    unknown = set(kw) - set(args)
+    if unknown:
+        raise TypeError(f"unexpected keyword arguments {sorted(unknown)}")
+    args.update(kw)
+    if args["save"]:
+        raise ValueError("save=True writes one set of files per solve: use sgp_betaDiv")
+    runs = _run(_B.BSGP_VARIANT_BETA, gn, psf, bkg, args["init_recon"], args["proj_type"],
+                args["stop_criterion"], args["MAXIT"], args["gamma"], args["beta"],
+                args["alpha"], args["alpha_min"], args["alpha_max"], args["M_alpha"],
+                args["tau"], args["M"], args["max_projs"], False, None, args["verbose"],
+                args["flux"], args["ccd_sat_level"], args["scale_data"], False,
+                args["tol_convergence"], args["use_original_SGP_Afunction"],
+                dict(bkw, betaParam=betas[0]), betas=betas)
+    cands = [(x, it, d, t, None) for x, it, d, t, _ in runs]
+    scores = [float(score(c[0])) if score is not None else float(c[2][-1]) for c in cands]
+    best = int(np.argmin(scores))
+    info = {"betas": betas, "scores": scores, "best_beta": betas[best], "candidates": cands}
+    if not final_solve:
+        return cands[best], info
+    final = sgp_betaDiv(gn, psf, bkg, betaParam=betas[best], **bkw, **kw)
+    return final, info

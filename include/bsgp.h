@@ -89,15 +89,31 @@ typedef struct {
                              recomputes the scaled gn/scaling (and the null-pixel fill)
                              on every read, bit-identical to f64 storage; the line
                              search reads half the bytes of gn. 0: f64 storage */
+  int32_t gn_f32;         /* 1: gn is the reference's float32 image (scale_data == 2: the
+                             caller scaled it in float32).  Under numpy 1.x promotion the
+                             beta objective then sums s*gn**beta as float32 terms
+                             (exponent rounded to float32) with numpy's float32 pairwise
+                             reduction, and rounds (s*beta)*gn to float32 before the
+                             multiply by den**(beta-1) (sgp.py:457-458); the device
+                             reproduces both.  With proj_type 0 the first iteration's
+                             scaling matrix clips to float32 bounds (sgp.py:726-729). */
+  int32_t beta0_general;  /* 1: every in->beta0[b] is neither 0 nor 1, so a batch with
+                             per-image betas can use the general-beta kernels */
 } bsgp_params;
+
+/* Storage of the per-image iteration vectors (bsgp_plan_create). */
+#define BSGP_STORAGE_F64 0
+#define BSGP_STORAGE_F32 1
 
 /* Device inputs of a batched solve. */
 typedef struct {
   const double* gn;    /* [B][H][W] observed images (any scale; scaled on device) */
   const double* bkg;   /* [B] or [B][H][W] (bkg_is_map)                           */
-  const double* flux;  /* [B] precomputed flux (unscaled) or NULL = sum(gn - bkg)  */
+  const double* flux;  /* [B] precomputed flux or NULL = sum(gn - bkg); unscaled, or
+                          already scaled when scale_data == 2 (sgp.py:208-211)      */
   const double* x0;    /* [B][H][W] initial x (init_recon == 1, or scale_data == 2), else NULL */
   const double* beta0; /* [B] per-image initial betaParam or NULL = params.betaParam */
+  const double* obj;   /* [B][H][W] ground truth (unscaled) for out->err, or NULL  */
 } bsgp_inputs;
 
 /* Device outputs of a batched solve.  MAXIT1 = MAXIT + 1. */
@@ -115,12 +131,21 @@ typedef struct {
                           from the small-step series, team size T, projection
                           passes over the image, projection-list entries read;
                           may be NULL */
+  double* err;         /* [B][MAXIT1] relative error ||x_k - obj|| / ||obj|| of the
+                          scaled iterate after the initial projection (k = 0) and after
+                          iteration k (errflag, sgp.py:240-257, 394-396); needs in->obj;
+                          may be NULL */
+  double* x_iter;      /* [B][MAXIT][H][W] the scaled iterate after each iteration,
+                          before the revert (save=True writes these, sgp.py:416-422);
+                          may be NULL */
 } bsgp_outputs;
 
 /* Plan: geometry, FFT sizes, twiddles and the PSF transfer functions for A and
- * AT, built on the device from the host PSF [kh][kw].  Synchronous. */
+ * AT, built on the device from the host PSF [kh][kw].  storage: BSGP_STORAGE_F64,
+ * or BSGP_STORAGE_F32 (iteration vectors kept in float32 in HBM, every sum and
+ * scalar in float64; SURVEY config C4).  Synchronous. */
 int bsgp_plan_create(int32_t H, int32_t W, const double* psf_host, int32_t kh, int32_t kw,
-                     int32_t conv_mode, int32_t device, bsgp_plan* out);
+                     int32_t conv_mode, int32_t storage, int32_t device, bsgp_plan* out);
 int bsgp_plan_destroy(bsgp_plan plan);
 /* FFT grid (P x Q) and the per-slot workspace bytes of the plan. */
 int bsgp_plan_info(bsgp_plan plan, int32_t* P, int32_t* Q, int64_t* slot_bytes,

@@ -241,6 +241,20 @@ def projectDF(b, c, dia, scaling, ccd_sat_level=None, lambda_=0, dlambda_=1, tol
 
 
 # ---------------------------------------------------------------------- solver
+def _np1_scalar_div(a, b):
+    """Scalar a / b under numpy 1.x promotion (the reference's numpy; this
+    module may run under numpy 2, whose NEP 50 rules differ for Python
+    scalars): scalar-with-scalar promotes by type, a Python float is float64."""
+    def dt(v):
+        if isinstance(v, (np.generic, np.ndarray)):
+            return np.asarray(v).dtype
+        return np.dtype(np.float64) if isinstance(v, float) else np.dtype(np.int64)
+    rt = np.promote_types(dt(a), dt(b))
+    if rt.kind != "f":
+        rt = np.dtype(np.float64)
+    return rt.type(np.asarray(a, dtype=rt) / np.asarray(b, dtype=rt))
+
+
 def _solve(gn, psf, bkg, *, variant, init_recon=0, proj_type=0, stop_criterion=0, MAXIT=500,
            gamma=1e-4, beta=0.4, alpha=1.3, alpha_min=1e-5, alpha_max=1e5, M_alpha=3, tau=0.5,
            M=1, max_projs=1000, verbose=True, flux=None, ccd_sat_level=None, scale_data=True,
@@ -266,8 +280,8 @@ def _solve(gn, psf, bkg, *, variant, init_recon=0, proj_type=0, stop_criterion=0
     elif init_recon == 2:
         x = gn.copy()
     else:
-        x = (np.sum(gn - bkg) / gn.size * np.ones_like(gn) if flux is None
-             else flux / gn.size * np.ones_like(gn))
+        x = (_np1_scalar_div(np.sum(gn - bkg), gn.size) * np.ones_like(gn) if flux is None
+             else _np1_scalar_div(flux, gn.size) * np.ones_like(gn))
     gn = gn.flatten()  # :180-182
     x = x.flatten()
     bkg = np.asarray(bkg).flatten()
@@ -276,14 +290,15 @@ def _solve(gn, psf, bkg, *, variant, init_recon=0, proj_type=0, stop_criterion=0
     elif stop_criterion in (2, 3):
         tol = tol_convergence
     elif stop_criterion == 4:
-        tol = 1 + 1 / np.mean(gn)
-    if scale_data:  # :193-199
+        tol = 1 + 1 / float(np.mean(gn))  # numpy 1.x: int / float32 scalar -> float64
+    if scale_data:  # :193-199 (arrays divided in their own dtype)
         scaling = np.max(gn)
         gn = gn / scaling
         bkg = bkg / scaling
         x = x / scaling
     else:
         scaling = 1.0
+    sc64 = float(scaling)  # numpy 1.x: Python scalars with the float32 scaling give float64
     vmin = np.min(gn[gn > 0])  # :202-204
     eps = np.finfo(float).eps
     gn[gn <= 0] = vmin * eps * eps
@@ -291,11 +306,11 @@ def _solve(gn, psf, bkg, *, variant, init_recon=0, proj_type=0, stop_criterion=0
     if flux is None:  # :208-211
         flux = np.sum(gn - bkg)
     else:
-        flux = flux / scaling
+        flux = _np1_scalar_div(flux, scaling)
     iter_ = 1
     Valpha = alpha_max * np.ones(M_alpha)
     Fold = -1e30 * np.ones(M)
-    Discr_coeff = 2 / N * scaling
+    Discr_coeff = 2 / N * sc64
     discr = np.zeros(MAXIT + 1)
     times = np.zeros(MAXIT + 1)
     E_p = 0
@@ -304,7 +319,7 @@ def _solve(gn, psf, bkg, *, variant, init_recon=0, proj_type=0, stop_criterion=0
     if proj_type == 0:  # :248-253
         x[x < 0] = 0
     else:
-        x = projectDF(flux, x, np.ones_like(x), scaling, ccd_sat_level=ccd_sat_level,
+        x = projectDF(flux, x, np.ones_like(x), sc64, ccd_sat_level=ccd_sat_level,
                       max_projs=max_projs)
     x_tf = A(x)  # :260-265 / :702-709
     den = x_tf + bkg
@@ -345,7 +360,7 @@ def _solve(gn, psf, bkg, *, variant, init_recon=0, proj_type=0, stop_criterion=0
             y[y < 0] = 0
         else:
             st = {}
-            y = projectDF(flux, np.multiply(y, D), D, scaling, ccd_sat_level=ccd_sat_level,
+            y = projectDF(flux, np.multiply(y, D), D, sc64, ccd_sat_level=ccd_sat_level,
                           max_projs=max_projs, stats=st)
             E_p += st["evals"]
         d = y - x

@@ -33,3 +33,25 @@ def ref_kwargs(fx):
 def ngc():
     d = golden("ngc7027_inputs.npz")
     return d["gn"], d["psf"], d["bg"][0][0], d["obj"]
+
+
+def app_case(name):
+    """Inputs + reference outputs of one application-path fixture
+    (tests/golden/make_golden.py app): the raw big-endian float32 image as
+    fits.getdata returns it (or the application's non-contiguous crop of a
+    wider frame), the >f8 DIAPL PSF, the background map, the flux in the
+    dtype the fixture was made with, and the application's kwargs."""
+    fx = golden(f"ref_{name}.npz")
+    kw = ref_kwargs(fx)
+    sub = golden("app_subdiv_inputs.npz")
+    if name.startswith("app_crop"):
+        crop = golden("app_crop_inputs.npz")
+        gn, bkg, flux = crop["wide"][:375, 75:], crop["bkg"], crop["flux"][()]
+    else:
+        gn, bkg, flux = sub["img"], sub["bkg"], sub["flux"][()]
+    kw["flux"] = np.float32(flux) if str(fx["flux_dtype"]) == "float32" else np.float64(flux)
+    return gn, sub["psf"], bkg, kw, str(fx["fn"]), fx
+
+
+APP_CASES = ["app_beta0", "app_beta1", "app_beta2", "app_beta3", "app_beta4", "app_kl",
+             "app_beta2_flux32", "app_crop_beta"]

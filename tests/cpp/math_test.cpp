@@ -43,6 +43,25 @@ int main() {
   printf("fast_exp max error %.3f ulp at t=%.17g\n", wexp, wexp_t);
   ok = ok && wexp < 1.0 && std::isinf(bsgp::fast_exp(1000.0)) && bsgp::fast_exp(-1000.0) == 0.0 &&
        std::isnan(bsgp::fast_exp(NAN));
+  // div_rn: the compact-gn decode gn/scaling (bsgp_math.hpp) must equal the
+  // IEEE quotient bit for bit for positive f32 numerators over a positive f32
+  // scaling (integer counts and general f32 FITS samples)
+  long ndiv = 0, bad_div = 0;
+  std::uniform_real_distribution<float> uf(1e-3f, 1e5f), us(1.0f, 7e4f);
+  std::uniform_int_distribution<int> ui(1, 70000);
+  for (int s = 0; s < 2000; ++s) {
+    const double sc = (s & 1) ? (double)us(rng) : (double)ui(rng);  // max(gn): f32-exact
+    const double r = 1.0 / sc;
+    for (int i = 0; i < 2000; ++i) {
+      const double a = (i & 1) ? (double)uf(rng) : (double)ui(rng);
+      ++ndiv;
+      if (bsgp::div_rn(a, sc, r) != a / sc) ++bad_div;
+    }
+    ++ndiv;
+    if (bsgp::div_rn(sc, sc, r) != 1.0) ++bad_div;  // the maximum pixel scales to exactly 1
+  }
+  printf("div_rn: %ld of %ld quotients differ from a / b\n", bad_div, ndiv);
+  ok = ok && bad_div == 0;
   printf(ok ? "math: all ok\n" : "math: FAIL\n");
   return ok ? 0 : 1;
 }

@@ -6,6 +6,7 @@ outputs); this script is how they were made:
 
     cd /root/repo && PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py circular
     cd /root/repo && PYTHONDONTWRITEBYTECODE=1 /opt/conda/bin/python3.9 tests/golden/make_golden.py linear
+    cd /root/repo && PYTHONDONTWRITEBYTECODE=1 /opt/conda/bin/python3.9 tests/golden/make_golden.py app
 
 * ``circular`` (py3.10, numpy 2.2): sgp / sgp_betaDiv with the original SGP
   Afunction (restoration/sgp.py:108-120), projectDF KATs
@@ -14,6 +15,17 @@ outputs); this script is how they were made:
   (restoration/simulated_test/data/*.mat).
 * ``linear`` (py3.9 + astropy 4.3.1): the astropy ``convolve_fft`` A/AT
   (restoration/sgp.py:121-161,583-615) and short linear-mode solves.
+* ``app`` (py3.9 + astropy 4.3.1, numpy 1.26): the drop-in's headline consumer,
+  restoration/application_sgp_subdivisions.py:43-107: the float32 big-endian
+  FITS subdivision results/SUBDIV_ORIGIMG.fits (375x375) as fits.getdata
+  returns it, the DIAPL PSF psf/psfccfbrd210048_1_1_img.fits (31x31, >f8), a
+  per-pixel background map, the provided flux, the application's kwargs, each
+  of the five beta seeds (:70-76) and the KL branch (:109-115); plus the
+  application's own non-contiguous crop img[:375, 75:] (:47) of the 450x450
+  results/CROWDED_SUBDIV_ORIGIMG.fits.  photutils is absent, so the
+  background map is a median-filtered, smoothed image (scipy.ndimage) and the
+  flux of the subdivision is the sum of the published restored image
+  results/SUBDIV_RESTOREDIMG_BETA.fits (the projection makes sum(x) == flux).
 
 The reference is imported unchanged; only its unused top-level imports
 (photutils, utils, and astropy where absent) are stubbed in ``sys.modules``.
@@ -332,6 +344,116 @@ def make_linear():
         print(f"{name:18s} {fn:12s} iters={it:3d} discr0={discr[0]:.10f} discrN={discr[-1]:.10f}")
 
 
+# --------------------------------------------------------------------------- errflag / save
+def make_errsave():
+    """sgp(errflag=True, obj, save=True) and sgp_betaDiv(save=True) on the
+    64x64 linear stamp: the err array (sgp.py:240-257, 394-396, 431-432) and
+    every FITS file the reference writes (orig, rec_k, res_k; sgp.py:223-231,
+    416-422), read back with astropy."""
+    import glob
+    from astropy.io import fits
+    sgp, fcp = import_reference(need_astropy=True)
+    gn64, psf9, obj = synth_field(64, 9, 25, seed=3)
+    app = dict(gamma=1e-4, beta=0.4, alpha_min=1e-5, alpha_max=1e5, alpha=10.0, M_alpha=3,
+               tau=0.5, M=1, proj_type=1, max_projs=1000, init_recon=2, ccd_sat_level=65000.0,
+               scale_data=True, use_original_SGP_Afunction=False)
+    out = {"gn": gn64, "psf": psf9, "obj": obj}
+    runs = {"kl": ("sgp", dict(app, stop_criterion=3, MAXIT=40, tol_convergence=1e-4,
+                               errflag=True, obj=obj, save=True)),
+            "beta": ("sgp_betaDiv", dict(app, stop_criterion=1, MAXIT=4, betaParam=1.05,
+                                         schedule_lr=True, adapt_beta=False, save=True,
+                                         errflag=True))}
+    for tag, (fn, kw) in runs.items():
+        d = tempfile.mkdtemp()
+        cwd = os.getcwd()
+        os.chdir(d)
+        try:
+            x, it, discr, _, err = run_quiet(getattr(sgp, fn), gn64, psf9, np.float64(100.0), **kw)
+            files = sorted(os.path.relpath(f, d) for f in glob.glob("SGP_reconstructed_images/*"))
+            for f in files:
+                key = os.path.basename(f).replace(".fits", "")
+                out[f"{tag}_{key}"] = fits.getdata(f).astype(np.float64)
+        finally:
+            os.chdir(cwd)
+        out[f"{tag}_files"] = np.array(files)
+        out[f"{tag}_x"], out[f"{tag}_iters"], out[f"{tag}_discr"] = x, it, discr
+        if err is not None:
+            out[f"{tag}_err"] = err
+        kws = {k: v for k, v in kw.items() if k != "obj"}
+        out[f"{tag}_kwargs"] = repr(kws)
+        out[f"{tag}_fn"] = fn
+        print(tag, fn, "iters", it, "files", len(files), "err", None if err is None else err[:4])
+    np.savez_compressed(os.path.join(OUT, "ref_errsave.npz"), **out)
+
+
+# --------------------------------------------------------------------------- app
+
+
+def app_betas():
+    """application_sgp_subdivisions.py:70-76."""
+    out = []
+    for seed in [0, 42, 951, 93, 810]:
+        np.random.seed(seed)
+        out.append(np.random.normal(loc=1, scale=0.05))
+    return out
+
+
+def app_kwargs(flux):
+    """application_sgp_subdivisions.py:17-20, 84-91 (DEFAULT_PARAMS unpacked)."""
+    return dict(gamma=1e-4, beta=0.4, alpha_min=1e-5, alpha_max=1e5, alpha=10.0, M_alpha=3,
+                tau=0.5, M=1, proj_type=1, max_projs=1000, init_recon=2, stop_criterion=3,
+                save=False, verbose=True, flux=flux, ccd_sat_level=65000, scale_data=True,
+                tol_convergence=1e-5, use_original_SGP_Afunction=False)
+
+
+def app_background(img):
+    from scipy import ndimage
+    return ndimage.gaussian_filter(
+        ndimage.median_filter(np.asarray(img, dtype=np.float64), size=61, mode="reflect"), 8.0)
+
+
+def make_app():
+    sgp, fcp = import_reference(need_astropy=True)
+    from astropy.io import fits
+    res = "/root/reference/results"
+    img = fits.getdata(os.path.join(res, "SUBDIV_ORIGIMG.fits"))  # (375, 375) >f4
+    psf = fits.getdata("/root/reference/psf/psfccfbrd210048_1_1_img.fits")  # (31, 31) >f8
+    bkg = app_background(img)
+    flux = np.float64(fits.getdata(os.path.join(res, "SUBDIV_RESTOREDIMG_BETA.fits")).sum())
+    assert img.dtype == np.dtype(">f4") and psf.dtype == np.dtype(">f8")
+    np.savez_compressed(os.path.join(OUT, "app_subdiv_inputs.npz"), img=img, psf=psf, bkg=bkg,
+                        flux=np.array(flux), betas=np.array(app_betas()))
+    runs = {}
+    for i, b in enumerate(app_betas()):
+        runs[f"app_beta{i}"] = (img, bkg, "sgp_betaDiv",
+                                dict(app_kwargs(flux), betaParam=b, lr=1e-3, lr_exp_param=0.1,
+                                     schedule_lr=True, adapt_beta=False))
+    runs["app_kl"] = (img, bkg, "sgp", app_kwargs(flux))
+    # the provided flux as a numpy float32 (flux /= scaling then runs in float32)
+    runs["app_beta2_flux32"] = (img, bkg, "sgp_betaDiv",
+                                dict(app_kwargs(np.float32(flux)), betaParam=app_betas()[2],
+                                     lr=1e-3, lr_exp_param=0.1, schedule_lr=True,
+                                     adapt_beta=False))
+    # the application's crop of a wider frame: a non-contiguous big-endian view
+    wide = fits.getdata(os.path.join(res, "CROWDED_SUBDIV_ORIGIMG.fits"))  # (450, 450) >f4
+    crop = wide[:375, 75:]
+    assert not crop.flags["C_CONTIGUOUS"] and crop.shape == (375, 375)
+    bkg_c = app_background(crop)
+    flux_c = np.float64(0.9 * np.sum(crop - bkg_c))
+    np.savez_compressed(os.path.join(OUT, "app_crop_inputs.npz"), wide=wide, bkg=bkg_c,
+                        flux=np.array(flux_c))
+    runs["app_crop_beta"] = (crop, bkg_c, "sgp_betaDiv",
+                             dict(app_kwargs(flux_c), betaParam=1.0248357076505616, lr=1e-3,
+                                  lr_exp_param=0.1, schedule_lr=True, adapt_beta=False))
+    for name, (g, bk, fn, kw) in runs.items():
+        x, it, discr, _, _ = run_quiet(getattr(sgp, fn), g, psf, bk, **kw)
+        kws = {k: v for k, v in kw.items() if k != "flux"}
+        np.savez_compressed(os.path.join(OUT, f"ref_{name}.npz"), x=x, iters=it, discr=discr,
+                            kwargs=repr(kws), fn=fn,
+                            flux_dtype=str(np.asarray(kw["flux"]).dtype))
+        print(f"{name:18s} {fn:12s} iters={it:3d} discr0={discr[0]:.10f} discrN={discr[-1]:.10f}")
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "circular"
     cwd = os.getcwd()
@@ -342,6 +464,10 @@ if __name__ == "__main__":
                 make_circular()
             elif which == "kats":
                 make_circular(solves_too=False)
+            elif which == "app":
+                make_app()
+            elif which == "errsave":
+                make_errsave()
             else:
                 make_linear()
         finally:

@@ -39,17 +39,19 @@ def test_library_exports_every_header_symbol():
 def test_ctypes_load_and_version():
     import _bsgp
     L = _bsgp.lib()
-    assert L.bsgp_abi_version() == 1
+    assert L.bsgp_abi_version() == 2
     for f in _bsgp.EXPORTED:
         assert hasattr(L, f)
     # argument validation runs on the host without a device
     h = __import__("ctypes").c_void_p()
     psf = np.ones((3, 3)) / 9.0
-    rc = L.bsgp_plan_create(8, 8, psf.ctypes.data, 3, 3, 0, 0, __import__("ctypes").byref(h))
+    rc = L.bsgp_plan_create(8, 8, psf.ctypes.data, 3, 3, 0, 0, 0, __import__("ctypes").byref(h))
     assert rc == -1 and b"psf.shape" in L.bsgp_last_error()
     bad = np.ones((8, 8))
-    rc = L.bsgp_plan_create(8, 8, bad.ctypes.data, 8, 8, 0, 0, __import__("ctypes").byref(h))
+    rc = L.bsgp_plan_create(8, 8, bad.ctypes.data, 8, 8, 0, 0, 0, __import__("ctypes").byref(h))
     assert rc == -4 and b"normalized" in L.bsgp_last_error()
+    rc = L.bsgp_plan_create(8, 8, psf.ctypes.data, 3, 3, 1, 7, 0, __import__("ctypes").byref(h))
+    assert rc == -1 and b"storage" in L.bsgp_last_error()
 
 
 def test_dropin_signatures_match_reference():
@@ -81,6 +83,12 @@ def test_dropin_errors_like_reference():
         sgp.sgp(gn, np.ones((8, 8)), np.float64(1.0))
     with pytest.raises(ValueError, match="errflag"):
         sgp.sgp(gn, np.ones((8, 8)) / 64, np.float64(1.0), errflag=True)
+    # sgp_betaDiv never checks errflag/obj (sgp.py:506-895 has no err path): the
+    # call goes on to the device, which is absent here
+    import _bsgp
+    if not (_bsgp.torch is not None and _bsgp.torch.cuda.is_available()):
+        with pytest.raises(_bsgp.BsgpError):
+            sgp.sgp_betaDiv(gn, np.ones((8, 8)) / 64, np.float64(1.0), errflag=True, MAXIT=2)
     assert sgp.lr_schedule(1e-3, 0.1, 3) == pytest.approx(1e-3 * np.exp(-0.3))
     assert sgp.betaDivDeriv(gn, gn, 1) == 0 and sgp.betaDivDeriv(gn, gn, 0) == 0
 
@@ -100,3 +108,18 @@ def test_product_never_imports_oracle():
     for fn in os.listdir(PKG):
         if fn.endswith(".py"):
             assert "sgp_oracle" not in open(os.path.join(PKG, fn)).read(), fn
+
+
+def test_check_status_raises_on_status_bits():
+    """counters[:, 3]: bit 4 (team barrier timed out) and bit 1 (line search
+    cap, only for a backtracking factor outside (0, 1)) are errors."""
+    import _bsgp
+    c = np.zeros((3, 8), np.int64)
+    _bsgp.check_status(c)
+    c[1, 3] = 4
+    with pytest.raises(_bsgp.BsgpError, match="barrier"):
+        _bsgp.check_status(c)
+    c[1, 3] = 1
+    with pytest.raises(_bsgp.BsgpError, match="line search"):
+        _bsgp.check_status(c)
+    assert _bsgp.BSGP_ERR_HIP == -2 and _bsgp.BSGP_ERR_ARG == -1

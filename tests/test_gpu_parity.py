@@ -319,3 +319,60 @@ def test_c4_field_2048_matches_oracle(sgpmod):
     assert it == itr
     assert rel(x, xr) < SOLVE_RTOL, rel(x, xr)
     np.testing.assert_allclose(d, dr, rtol=1e-7)
+
+
+# ------------------------------------------------ the timed configuration
+def test_bench_c3_path_exact(sgpmod):
+    """bench.py's timed path itself: BASELINE config C3 (1024 x 256x256,
+    beta 1.05, 25x25 PSF, linear A, projection), the bench generator's inputs,
+    team 1 (auto for 1024 images), the default 3 sub-batch streams and
+    gn_compact on, for 10 iterations.  All 1024 images: finite, x >= 0,
+    sum(x) == flux.  Image 0 is replaced by the reference's lin256_beta input
+    and matches its golden output; 8 sampled images are bitwise equal to
+    single-image solves, with gn_compact on and off."""
+    import torch
+
+    import bench
+    bench.torch = torch
+    B = 1024
+    gn, psf = bench.synth_batch(B, 256, 25, 200, seed0=0)
+    fx = golden("ref_lin256_beta.npz")
+    np.testing.assert_allclose(psf, fx["psf"], rtol=1e-15)
+    gn[0] = torch.from_numpy(fx["gn"].astype(np.float64)).cuda()
+    bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
+    kw = bench.solve_kwargs(10, None)
+    assert kw["streams"] is None and kw["team"] is None and sgpmod.STREAMS_DEFAULT == 3
+    assert sgpmod.GN_COMPACT_DEFAULT == 1
+    out = sgpmod.sgp_betaDiv_batch(gn, psf, bkg, **kw)
+    x = out["x"]
+    assert np.all(out["counters"][:, 5] == 1) and np.all(out["counters"][:, 3] == 0)
+    assert np.all(out["iters"] == 10)
+    assert np.all(np.isfinite(x)) and np.all(x >= 0)
+    g = gn.cpu().numpy()
+    flux = np.sum(g - 100.0, axis=(1, 2))
+    np.testing.assert_allclose(x.sum(axis=(1, 2)), flux, rtol=1e-9)
+    assert rel(x[0], fx["x"]) < SOLVE_RTOL, rel(x[0], fx["x"])
+    np.testing.assert_allclose(out["discr"][0, :11], fx["discr"], rtol=1e-7)
+    for i in (1, 137, 341, 511, 512, 700, 1000, 1023):
+        for compact in (1, 0):
+            one = sgpmod.sgp_betaDiv_batch(gn[i:i + 1], psf, bkg[i:i + 1],
+                                           **dict(kw, team=1, streams=1, gn_compact=compact))
+            assert one["iters"][0] == out["iters"][i]
+            np.testing.assert_array_equal(one["x"][0], x[i])
+            np.testing.assert_array_equal(one["discr"][0], out["discr"][i])
+
+
+def test_gn_compact_is_bitwise_neutral(sgpmod):
+    """gn_compact 1 (observed counts kept in f32, decoded on every read) and 0
+    (f64 storage) give the same bits, for one-workgroup and team solves."""
+    fx = golden("ref_lin64_beta.npz")
+    gn = fx["gn"].astype(np.float64)
+    gns = np.stack([gn, np.roll(gn, 9, 1), gn.T.copy()])
+    kw = dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=15, alpha=10.0,
+              ccd_sat_level=65000.0, use_original_SGP_Afunction=False, schedule_lr=True,
+              adapt_beta=False, betaParams=1.05)
+    for team in (1, 4):
+        a = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, team=team, gn_compact=1, **kw)
+        b = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, team=team, gn_compact=0, **kw)
+        np.testing.assert_array_equal(a["x"], b["x"])
+        np.testing.assert_array_equal(a["discr"], b["discr"])

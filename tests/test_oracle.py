@@ -90,3 +90,76 @@ def test_oracle_linear_solves(name):
     rel = np.linalg.norm(x - fx["x"]) / np.linalg.norm(fx["x"])
     assert rel < 1e-8, rel
     np.testing.assert_allclose(discr, fx["discr"], rtol=1e-8)
+
+
+# ------------------------------------------------- application drop-in path
+from conftest import APP_CASES, app_case  # noqa: E402
+
+
+@pytest.mark.parametrize("name", APP_CASES)
+def test_oracle_application_path(name):
+    """application_sgp_subdivisions.py:43-107 on float32 big-endian FITS data
+    (incl. the non-contiguous crop) with a background map and provided flux:
+    the oracle follows the reference's float32 arithmetic (numpy 1.x rules)."""
+    gn, psf, bkg, kw, fn, fx = app_case(name)
+    assert gn.dtype == np.dtype(">f4")
+    x, it, discr, _, _ = getattr(orc, fn)(gn, psf, bkg, **kw)
+    assert it == int(fx["iters"])
+    rel = np.linalg.norm(x - fx["x"]) / np.linalg.norm(fx["x"])
+    assert rel < 1e-8, rel
+    np.testing.assert_allclose(discr, fx["discr"], rtol=1e-9)
+
+
+def _pairwise_model(a, prog, counts):
+    """Evaluates the plans' numpy float32 reduction program (bsgp_api.hip
+    pairwise_program) in float32, the way the setup kernel does."""
+    nleaf, nnode, nlev, nchunk = counts
+    lv = prog[:2 * nleaf].reshape(-1, 2)
+    nd = prog[2 * nleaf:2 * (nleaf + nnode)].reshape(-1, 2)
+    off = prog[2 * (nleaf + nnode):2 * (nleaf + nnode) + nlev + 1]
+    roots = prog[2 * (nleaf + nnode) + nlev + 1:]
+    vals = np.zeros(nleaf + nnode, np.float32)
+    for l, (s0, n) in enumerate(lv):
+        t = a[s0:s0 + n]
+        if n < 8:
+            r = np.float32(0)
+            for v in t:
+                r = np.float32(r + v)
+        else:
+            acc = t[:8].copy()
+            i = 8
+            while i < n - n % 8:
+                acc = (acc + t[i:i + 8]).astype(np.float32)
+                i += 8
+            r = np.float32(np.float32(np.float32(acc[0] + acc[1]) + np.float32(acc[2] + acc[3]))
+                           + np.float32(np.float32(acc[4] + acc[5]) + np.float32(acc[6] + acc[7])))
+            for v in t[i:]:
+                r = np.float32(r + v)
+        vals[l] = r
+    for h in range(nlev):
+        for k in range(off[h], off[h + 1]):
+            vals[nleaf + k] = np.float32(vals[nd[k, 0]] + vals[nd[k, 1]])
+    r = np.float32(0)
+    for c in roots:
+        r = np.float32(r + vals[c])
+    return r
+
+
+@pytest.mark.parametrize("n", [1, 5, 8, 127, 128, 129, 1000, 8192, 8193, 16391, 65537, 140625])
+def test_numpy_f32_sum_model(n):
+    """The float32 reduction order the device reproduces for gn_f32 solves
+    (np.sum of the float32 terms s*gn**beta, sgp.py:458) equals numpy's own
+    np.sum bit for bit."""
+    import ctypes
+    import _bsgp
+    L = _bsgp.lib()
+    L.bsgp_pairwise_program.restype = ctypes.c_int64
+    L.bsgp_pairwise_program.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                        ctypes.c_void_p]
+    counts = np.zeros(4, np.int32)
+    m = L.bsgp_pairwise_program(n, None, 0, counts.ctypes.data)
+    prog = np.zeros(m, np.int32)
+    L.bsgp_pairwise_program(n, prog.ctypes.data, m, counts.ctypes.data)
+    for seed in range(3):
+        a = np.random.default_rng(1000 * n + seed).uniform(-1, 3, n).astype(np.float32)
+        assert _pairwise_model(a, prog, counts) == np.sum(a)
