@@ -1103,8 +1103,8 @@ struct Objective {
   int mode;             // 0 KL, 1 beta=0, 2 beta=1, 3 general
   // float32 observed image (params.gn_f32): numpy 1.x evaluates (s*b)*gn as
   // float32(s*b) * gn in float32 before the float64 multiply (sgp.py:458)
-  bool f32g;
-  float c2f;
+  bool f32g = false;
+  float c2f = 0.0f;
   __device__ __forceinline__ void set_beta(double b) {
     beta = b;
     if (variant == 0) {

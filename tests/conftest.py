@@ -55,3 +55,25 @@ def app_case(name):
 
 APP_CASES = ["app_beta0", "app_beta1", "app_beta2", "app_beta3", "app_beta4", "app_kl",
              "app_beta2_flux32", "app_crop_beta"]
+
+
+def konst_shift(gn, kw, fx):
+    """Discrepancy offset between the device and a float32-image reference run
+    that comes only from numpy's float32 power.  The beta objective's constant
+    K = np.sum(s * gn**beta) is a float32 sum of float32 terms (sgp.py:458);
+    numpy evaluates float32 ** on AVX-512 CPUs with SVML, which is not
+    correctly rounded, while the device rounds the exact power to float32.
+    Both then sum in numpy's order (tests/test_oracle.py::
+    test_numpy_f32_sum_model), so their K differ by at most an ulp or two of
+    float32, and the discrepancy 2/N*scaling*f by that constant.  Returns
+    2/N*scaling*(K_device - K_reference), K_device restated here with the
+    exact power; 0 for KL runs."""
+    if str(fx["fn"]) != "sgp_betaDiv" or "konst" not in fx:
+        return 0.0
+    g = np.asarray(gn).astype(np.float32).reshape(-1)
+    sc = np.max(g)
+    gs = g / sc
+    b = float(kw["betaParam"])
+    p = (gs.astype(np.float64) ** np.float64(np.float32(b))).astype(np.float32)
+    k_dev = np.sum(np.float32(1 / (b * (b - 1))) * p)
+    return 2 / g.size * float(sc) * (float(k_dev) - float(fx["konst"]))

@@ -448,9 +448,19 @@ def make_app():
     for name, (g, bk, fn, kw) in runs.items():
         x, it, discr, _, _ = run_quiet(getattr(sgp, fn), g, psf, bk, **kw)
         kws = {k: v for k, v in kw.items() if k != "flux"}
+        extra = {}
+        if fn == "sgp_betaDiv":
+            # the float32 constant of betaDiv (sgp.py:458) exactly as the reference
+            # evaluates it on the scaled image (sgp.py:634, 649-650): numpy's float32
+            # power here is not correctly rounded (AVX-512 SVML), so this value is
+            # kept to separate that rounding from the engine's
+            b = kw["betaParam"]
+            gs = g.flatten() / np.max(g.flatten())
+            extra["konst"] = np.sum(1 / (b * (b - 1)) * gs ** b)
+            assert extra["konst"].dtype == np.float32
         np.savez_compressed(os.path.join(OUT, f"ref_{name}.npz"), x=x, iters=it, discr=discr,
                             kwargs=repr(kws), fn=fn,
-                            flux_dtype=str(np.asarray(kw["flux"]).dtype))
+                            flux_dtype=str(np.asarray(kw["flux"]).dtype), **extra)
         print(f"{name:18s} {fn:12s} iters={it:3d} discr0={discr[0]:.10f} discrN={discr[-1]:.10f}")
 
 
