@@ -1,30 +1,39 @@
 """Benchmark: SGP iterations/s (fp64) on batched 256x256 images + %HBM peak.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c1] ...
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5] ...
 
 A *step* is one complete batched solve (BASELINE config C3: 1024 independent
-256x256 star-field stamps, beta-SGP, fp64, 25x25 Gaussian PSF with the
+256x256 star-field stamps per GPU, beta-SGP, fp64, 25x25 Gaussian PSF with the
 astropy-semantics linear A, flux-conserving projection, MAXIT iterations with
 stop_criterion=1 so every image runs exactly MAXIT iterations).
 Inputs are synthetic (SURVEY §8d generator), built on the device and resident
 in HBM before timing starts.  ``value`` = image-iterations of all ranks /
-max-over-ranks wall time of the K timed steps.  Multi-GPU: one process per
-GPU, each rank solves its own batch (seeds offset by rank): weak scaling, no
-collective on the data path.
+max-over-ranks wall time of the K timed steps.
 
-roofline: algorithmic bytes of the passes the engine makes over HBM-resident
-image vectors (8*N*(23 + 2*proj_passes + 3*ls_passes) per image-iteration plus
-16 B per projection-list entry read, all counted on the device; SURVEY §8d's
-per-evaluation formula is reported beside it) / the solve's duration measured
-with HIP events on the launch stream (the solve is the unit launched: setup +
-MAXIT x five phase kernels on three sub-batch streams); peak 8.0 TB/s.
-traffic: HBM bytes per solve from a rocprofv3 PMC run (profiles/), if present.
+Multi-GPU: one process per GPU.  Under torchrun the ranks come
+from RANK/LOCAL_RANK/WORLD_SIZE; ``--gpus N`` without torchrun starts the N
+rank processes itself (before this process touches a GPU).  Each rank solves
+its own shard of independent images with no collective on the data path; the
+harness's barrier and its max/sum of two scalars run over gloo (CPU).  C3 is
+weak scaling (1024 images per GPU); C5 is BASELINE config 5, 8192 images
+split over the ranks (strong scaling; 1024 per GPU at N=8).
+
+roofline: from a profiled solve after the timed loop (one stream, a HIP event
+pair around every kernel launch, bsgp_solve_profiled): each kernel class's
+span per launch and its algorithmic bytes per launch (the HBM bytes of the
+passes that kernel makes, from the device's pass counters); the
+reported kernel is the one with the largest share of the solve.  traffic:
+PMC-measured HBM bytes per launch of that kernel (profiles/traffic_<config>.json,
+scripts/gpu_traffic.sh) when present.
 cpu_baseline: the numpy oracle (oracle/sgp_oracle.py, a port of the reference)
-on a bounded sample of the same workload, process pool on this host's cores.
+on a bounded sample of the same workload, a process pool on this host's cores
+(capped at the 16 cores a one-GPU share of the box has).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -39,6 +48,7 @@ torch = None  # imported in main() before libbsgp (one HIP runtime per process);
 #               out of module scope so spawned CPU-baseline workers stay light
 
 HBM_PEAK_GBS = 8000.0
+CPU_CAP = 16  # host cores of a one-GPU share of the box
 
 
 def gaussian_psf(k, fwhm=None):
@@ -60,8 +70,8 @@ def embed_psf(psf, n):
     return full / full.sum()
 
 
-# SURVEY §8d configurations that fit one GPU (C1 is the reference's own
-# NGC7027 CPU case; C5 is C3 sharded over 8 GPUs = `--config c3 --gpus 8`).
+# SURVEY §8d configurations (C1 is the reference's own NGC7027 CPU case).
+# batch: images per GPU (weak scaling); total: images of the whole job (strong).
 CONFIGS = {
     "c2": dict(n=256, k=25, nstars=200, batch=1, circular=False,
                desc="single {n}x{n} synthetic image, 25x25 Gaussian PSF, linear A"),
@@ -70,6 +80,9 @@ CONFIGS = {
     "c4": dict(n=2048, k=64, nstars=5000, batch=1, circular=True,
                desc="single {n}x{n} synthetic field, 64x64 PSF embedded at the centre, "
                     "circular A (pow-2 FFT)"),
+    "c5": dict(n=256, k=25, nstars=200, total=8192, circular=False,
+               desc="{T} independent {n}x{n} subdivisions split over the GPUs ({B} on this "
+                    "rank), 25x25 PSF, linear A"),
 }
 
 
@@ -109,6 +122,16 @@ def solve_kwargs(maxit, ls_spec, streams=None, team=None, circular=False, proj_c
                 team=team, proj_cache=proj_cache)
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(n, k, nstars, images, maxit, workers, circular=False):
     """Oracle (numpy port of the reference, oracle/sgp_oracle.py) on `images`
     stamps x `maxit` iterations, one image per task on `workers` processes;
@@ -118,11 +141,14 @@ def cpu_baseline(n, k, nstars, images, maxit, workers, circular=False):
     for key in ("ls_spec", "team", "streams", "proj_cache"):
         kw.pop(key)
     iters, wall, cpu_s = cpu_bench.run_pool(n, k, nstars, images, kw, workers)
+    ncpu = os.cpu_count() or 1
     return {"value": iters / wall, "unit": "image-iterations/s", "cores": workers,
             "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": ncpu,
             "sample": f"{images} images {n}x{n} (bench generator) x {maxit} beta-SGP iterations "
-                      f"with oracle/sgp_oracle.py on a pool of {workers} processes: "
-                      f"{iters} image-iterations in {wall:.1f}s wall "
+                      f"with oracle/sgp_oracle.py, one image per process on {workers} processes "
+                      f"({cpu_model()}; the host shows {ncpu} CPUs, a one-GPU share is "
+                      f"{CPU_CAP}): {iters} image-iterations in {wall:.1f}s wall "
                       f"({iters / cpu_s:.1f} image-it/s per core)"}
 
 
@@ -132,17 +158,76 @@ def shard_seed0(rank, images_per_rank):
     return rank * images_per_rank
 
 
-def aggregate(dist, elapsed, iters_sum, device):
+def shard_bounds(total, world, rank):
+    """Contiguous shard [lo, hi) of `total` images for `rank` of `world` (C5)."""
+    return total * rank // world, total * (rank + 1) // world
+
+
+def aggregate(dist, elapsed, iters_sum, device="cpu"):
     """Cross-rank reduction of one timed run: the max wall time over ranks and
     the total image-iterations of all ranks (the only collectives of the
-    harness).  Works with any torch.distributed backend (nccl on the GPU box,
-    gloo in the CPU tests)."""
+    harness, on CPU tensors over gloo)."""
     t = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
     n = torch.tensor([float(iters_sum)], dtype=torch.float64, device=device)
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(n, op=dist.ReduceOp.SUM)
     return float(t.item()), float(n.item())
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` without torchrun: start one rank process per GPU (this
+    process has not touched a GPU), wait for all, return the worst exit code.
+    Rank 0 prints the JSON line."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def kernel_bytes(H, W, P, Qh, counters, iters, beta, series, compact, bmap, fused_at_col):
+    """Algorithmic HBM bytes of each kernel class over one solve: the passes
+    each kernel makes over the per-image vectors (counted on the device) plus
+    its spectrum traffic.  N = H*W pixels; S = 16*H*Qh bytes of
+    stored half spectrum; TF = 16*P*Qh bytes of transfer function.
+      k_dir: (x, g) per projection pass + 16 B per list entry read; (x, g)
+             for the direction and its row transforms; writes the spectrum.
+      k_col: reads and writes the spectrum, reads the TF (A; AT too if unfused).
+      k_ls:  pass 1 reads the spectrum, x_tf, gn, pw (series) [, bkg map] and
+             writes d_tf; every further pass reads x_tf, d_tf, gn [, bkg];
+             accept reads the same, writes x_tf, pw (beta) and the spectrum;
+             AT's column pass (fused for one-workgroup images).
+      k_bb:  reads the spectrum, pw (beta), x, g; writes x, g."""
+    N = float(H * W)
+    S, TF = 16.0 * H * Qh, 16.0 * P * Qh
+    gb = 4.0 if compact else 8.0
+    bb = 8.0 if bmap else 0.0
+    it = float(np.sum(iters))
+    proj_passes, list_reads = float(np.sum(counters[:, 6])), float(np.sum(counters[:, 7]))
+    ls_passes = float(np.sum(counters[:, 2]))
+    b = {}
+    b["k_dir"] = 16.0 * N * proj_passes + 16.0 * list_reads + it * (16.0 * N + S)
+    col_per = 2.0 * S + TF
+    b["k_ls"] = (it * (S + N * (8.0 + gb + (8.0 if series else 0.0) + bb) + 8.0 * N)
+                 + (ls_passes - it) * N * (16.0 + gb + bb)
+                 + it * (N * (16.0 + gb + bb) + N * (16.0 if beta else 8.0) + S)
+                 + (it * col_per if fused_at_col else 0.0))
+    b["k_bb"] = it * (S + N * ((8.0 if beta else 0.0) + 16.0) + 16.0 * N)
+    b["k_col"] = it * col_per * (1.0 if fused_at_col else 2.0)
+    return b
 
 
 def load_traffic(config):
@@ -155,24 +240,36 @@ def load_traffic(config):
     return None
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (c2/c3/c4)")
     ap.add_argument("--maxit", type=int, default=100)
     ap.add_argument("--ls-spec", type=int, default=None)
     ap.add_argument("--streams", type=int, default=None)
     ap.add_argument("--team", type=int, default=None,
                     help="workgroups per image (0/None = auto, 1 = one per image)")
-    ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--proj-cache", type=int, default=None)
+    ap.add_argument("--storage", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="skip the profiled solve (per-kernel roofline)")
     ap.add_argument("--cpu-images", type=int, default=16)
     ap.add_argument("--cpu-maxit", type=int, default=None,
                     help="iterations per CPU-baseline image (default: --maxit)")
-    args = ap.parse_args()
+    ap.add_argument("--stub", action="store_true",
+                    help="harness only, no GPU: a fixed CPU wait stands in for each solve "
+                         "(tests of the multi-rank path)")
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     global torch
     import torch as _torch
     torch = _torch
@@ -180,72 +277,80 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
-
-    import _bsgp
-    import sgp
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     cfg = CONFIGS[args.config]
     n, k, nstars, circ = cfg["n"], cfg["k"], cfg["nstars"], cfg["circular"]
-    B = args.batch if args.batch else cfg["batch"]
-    gn, psf = synth_batch(B, n, k, nstars, seed0=shard_seed0(rank, B), circular=circ)
-    bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
+    strong = "total" in cfg
+    if strong:
+        lo, hi = shard_bounds(cfg["total"], world, rank)
+        B, seed0 = hi - lo, lo
+    else:
+        B = args.batch if args.batch else cfg["batch"]
+        seed0 = shard_seed0(rank, B)
     kw = solve_kwargs(args.maxit, args.ls_spec, args.streams, args.team, circular=circ,
                       proj_cache=args.proj_cache)
-    torch.cuda.synchronize()
 
-    def step():
-        return sgp.sgp_betaDiv_batch(gn, psf, bkg, device_out=True, **kw)
+    if args.stub:
+        def step():
+            time.sleep(0.01)
+            return {"iters": np.full(B, args.maxit)}
+
+        def sync():
+            pass
+    else:
+        torch.cuda.set_device(local)
+        import _bsgp
+        import sgp
+        gn, psf = synth_batch(B, n, k, nstars, seed0=seed0, circular=circ)
+        bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()
+
+        def step():
+            return sgp.sgp_betaDiv_batch(gn, psf, bkg, device_out=True, **kw)
+
+        def sync():
+            torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         out = step()
-    torch.cuda.synchronize()
+    sync()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     ev = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        if args.stub:
+            out = step()
+            continue
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
         out = step()
         e1.record()
         ev.append((e0, e1))
-    torch.cuda.synchronize()
+    sync()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    iters = out["iters"].cpu().numpy()
-    cnt = out["counters"].cpu().numpy()
-    elapsed_max, tot = aggregate(dist, elapsed, iters.sum(), "cuda")
+    iters = out["iters"].cpu().numpy() if torch.is_tensor(out["iters"]) else out["iters"]
+    elapsed_max, tot = aggregate(dist, elapsed, iters.sum())
     total_iters = tot * args.steps
     value = total_iters / elapsed_max
+    if dist:
+        dist.destroy_process_group()
+    if rank != 0:
+        return
 
-    # Algorithmic bytes per solve, b = 0 (scalar background).  SURVEY §8d
-    # prices every projection / line-search *evaluation* as a pass over the
-    # image: 8*N*(23 + 2*E_p + 3*E_ls) per image-iteration.  The engine needs
-    # fewer passes (line-search trials from the moment series, several trials
-    # per pass, projection evaluations from the pixel lists), so the roofline
-    # uses the bytes of the passes it actually makes:
-    #   8*N*(23 + 2*proj_passes + 3*ls_passes) + 16*(list entries read).
-    N = n * n
-    E_p, E_ls = cnt[:, 0].astype(np.float64), cnt[:, 1].astype(np.float64)
-    ls_passes = cnt[:, 2].astype(np.float64)
-    proj_passes, list_reads = cnt[:, 6].astype(np.float64), cnt[:, 7].astype(np.float64)
-    survey_bytes = float(np.sum(8.0 * N * (23.0 * iters + 2.0 * E_p + 3.0 * E_ls)))
-    alg_bytes = float(np.sum(8.0 * N * (23.0 * iters + 2.0 * proj_passes + 3.0 * ls_passes)
-                             + 16.0 * list_reads))
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = load_traffic(args.config)
+    workload = (f"{args.config.upper()}: "
+                + cfg["desc"].format(n=n, B=B, T=cfg.get("total", B))
+                + f", beta-SGP (beta=1.05), proj_type=1, MAXIT={args.maxit}, stop_criterion=1")
     result = {
         "metric": "SGP iterations/sec (fp64) on batched 256x256 images",
         "value": value,
@@ -255,46 +360,96 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed_max / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SURVEY §8d generator: pareto point sources * 25x25 Gaussian PSF "
                 "+ Poisson, bkg 100), built on device",
-        "config": {"workload": f"{args.config.upper()}: " + cfg["desc"].format(n=n, B=B)
-                               + f", beta-SGP (beta=1.05), proj_type=1, "
-                               f"MAXIT={args.maxit}, stop_criterion=1",
-                   "images_per_gpu": B, "image": [n, n], "psf": [k, k], "maxit": args.maxit,
-                   "parallelism": f"{world} independent shards (no collective)",
-                   "ls_spec": kw["ls_spec"] or sgp.LS_SPEC_DEFAULT,
-                   "streams": kw["streams"] or sgp.STREAMS_DEFAULT,
-                   "team": int(cnt[0, 5]),
-                   "proj_cache": kw["proj_cache"] if kw["proj_cache"] is not None
-                   else sgp.PROJ_CACHE_DEFAULT},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic.get("bytes_per_launch") if traffic else None,
-                     "kernel": "one solve = setup + MAXIT x (k_dir, k_col, k_ls, k_col, k_bb)",
-                     "kernel_ms": kern_ms,
-                     "alg_bytes_per_launch": alg_bytes,
-                     "survey_formula_bytes_per_launch": survey_bytes,
-                     "E_p_per_iter": float(E_p.sum() / iters.sum()),
-                     "E_ls_per_iter": float(E_ls.sum() / iters.sum()),
-                     "proj_passes_per_iter": float(proj_passes.sum() / iters.sum()),
-                     "proj_list_frac_per_iter": float(list_reads.sum() / iters.sum() / N),
-                     "ls_passes_per_iter": float(ls_passes.sum() / iters.sum()),
-                     "ls_series_per_iter": float(cnt[:, 4].sum() / iters.sum())},
+        "config": {"workload": workload, "images_per_gpu": B,
+                   "images_total": cfg.get("total", B * world), "image": [n, n], "psf": [k, k],
+                   "maxit": args.maxit,
+                   "parallelism": f"{world} independent shards, one process per GPU "
+                                  f"(no collective on the data path)"},
+        "roofline": None,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
-        workers = max(1, min(16, os.cpu_count() or 1))
+    if args.stub:
+        result["data"] = "stub: harness test without a GPU"
+        print(json.dumps(result), flush=True)
+        return
+
+    import sgp
+    cnt = out["counters"].cpu().numpy()
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    result["config"].update({"ls_spec": kw["ls_spec"] or sgp.LS_SPEC_DEFAULT,
+                             "streams": kw["streams"] or sgp.STREAMS_DEFAULT,
+                             "team": int(cnt[0, 5]),
+                             "proj_cache": kw["proj_cache"] if kw["proj_cache"] is not None
+                             else sgp.PROJ_CACHE_DEFAULT,
+                             "gn_compact": sgp.GN_COMPACT_DEFAULT, "storage": args.storage})
+    if not args.no_profile:
+        result["roofline"] = roofline(args, kw, gn, psf, bkg, B, n, kern_ms)
+    if world == 1 and not args.no_cpu:
+        workers = max(1, min(CPU_CAP, os.cpu_count() or 1))
         images = args.cpu_images if B > 1 else 1
         cpu_maxit = args.cpu_maxit if args.cpu_maxit else args.maxit
         result["cpu_baseline"] = cpu_baseline(n, k, nstars, images, cpu_maxit,
                                               min(workers, images), circular=circ)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    print(json.dumps(result), flush=True)
+
+
+def roofline(args, kw, gn, psf, bkg, B, n, solve_ms):
+    """Per-kernel roofline from one profiled solve (outside the timed loop)."""
+    import _bsgp
+    import sgp
+    prof = sgp.sgp_betaDiv_batch(gn, psf, bkg, profile=True, **kw)
+    plan = _bsgp.get_plan(n, n, psf, _bsgp.BSGP_CONV_CIRCULAR if kw["use_original_SGP_Afunction"]
+                          else _bsgp.BSGP_CONV_LINEAR_FILL)
+    cnt, iters = prof["counters"], prof["iters"]
+    team = int(cnt[0, 5])
+    kb = kernel_bytes(n, n, plan.P, plan.Q // 2 + 1, cnt, iters, beta=True, series=True,
+                      compact=sgp.GN_COMPACT_DEFAULT == 1, bmap=False,
+                      fused_at_col=(team == 1))
+    names = ["k_setup", "k_dir", "k_col", "k_ls", "k_bb"]
+    ms, nl = prof["kernel_ms"], prof["launches"]
+    kernels = {}
+    for i, name in enumerate(names):
+        if i == 0 or nl[i] == 0:
+            kernels[name] = {"ms_total": float(ms[i]), "launches": int(nl[i])}
+            continue
+        per_ms = ms[i] / nl[i]
+        per_b = kb[name] / nl[i]
+        ach = per_b / (per_ms * 1e-3) / 1e9
+        kernels[name] = {"ms_total": float(ms[i]), "launches": int(nl[i]),
+                         "ms_per_launch": float(per_ms), "bytes_per_launch": float(per_b),
+                         "achieved": float(ach), "frac": float(ach / HBM_PEAK_GBS)}
+    dom = max(names[1:], key=lambda k_: kernels[k_]["ms_total"])
+    d = kernels[dom]
+    prof_total = float(np.sum(ms))
+    alg_total = float(sum(kb.values()))
+    traffic = load_traffic(args.config)
+    tr = None
+    if traffic and isinstance(traffic.get("kernels"), dict) and dom in traffic["kernels"]:
+        tr = traffic["kernels"][dom].get("bytes_per_launch")
+    return {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": d["frac"], "traffic": tr,
+            "ms_per_launch": d["ms_per_launch"], "bytes_per_launch": d["bytes_per_launch"],
+            "launch_unit": f"one launch = {B} images x one iteration of {dom} "
+                           f"(profiled solve on one stream)",
+            "kernels": kernels,
+            "profiled_solve_ms": prof_total,
+            "solve": {"alg_bytes": alg_total, "ms_timed": solve_ms,
+                      "achieved_timed": alg_total / (solve_ms * 1e-3) / 1e9,
+                      "frac_timed": alg_total / (solve_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                      "note": "whole solve in the timed loop (sub-batch streams overlap "
+                              "kernels), same bytes"},
+            "counters_per_iter": {
+                "E_p": float(cnt[:, 0].sum() / iters.sum()),
+                "E_ls": float(cnt[:, 1].sum() / iters.sum()),
+                "proj_passes": float(cnt[:, 6].sum() / iters.sum()),
+                "proj_list_frac": float(cnt[:, 7].sum() / iters.sum() / (n * n)),
+                "ls_passes": float(cnt[:, 2].sum() / iters.sum()),
+                "ls_series": float(cnt[:, 4].sum() / iters.sum())}}
 
 
 if __name__ == "__main__":

@@ -108,6 +108,7 @@ def lib():
             L.bsgp_plan_info.argtypes = [vp, vp, vp, vp, vp]
             L.bsgp_solve_device.argtypes = [vp, i32, vp, vp, vp, vp]
             L.bsgp_solve_host.argtypes = [vp, i32, vp, vp, vp]
+            L.bsgp_solve_profiled.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
             L.bsgp_apply_operator.argtypes = [vp, i32, i32, vp, vp, vp]
             L.bsgp_project_df.argtypes = [i64, dbl, vp, vp, dbl, i32, dbl, dbl, dbl, dbl, i32,
                                           i32, i32, vp, vp, vp]
@@ -120,7 +121,8 @@ def lib():
             L.bsgp_psf_stamps.argtypes = [ctypes.POINTER(PsfModel), vp, i32, i32, i32, vp, vp]
             L.bsgp_plan_set_psfs.argtypes = [vp, vp, i32, vp]
             for name in ["bsgp_plan_create", "bsgp_plan_destroy", "bsgp_plan_info",
-                         "bsgp_solve_device", "bsgp_solve_host", "bsgp_apply_operator",
+                         "bsgp_solve_device", "bsgp_solve_host", "bsgp_solve_profiled",
+                         "bsgp_apply_operator",
                          "bsgp_project_df", "bsgp_beta_div", "bsgp_beta_div_deriv",
                          "bsgp_beta_div_grad_parts", "bsgp_device_synchronize",
                          "bsgp_extract_tiles", "bsgp_coadd_tiles", "bsgp_fits_to_f64",
@@ -134,7 +136,7 @@ def lib():
 
 
 EXPORTED = ["bsgp_plan_create", "bsgp_plan_destroy", "bsgp_plan_info", "bsgp_solve_device",
-            "bsgp_solve_host", "bsgp_apply_operator", "bsgp_project_df", "bsgp_beta_div",
+            "bsgp_solve_host", "bsgp_solve_profiled", "bsgp_apply_operator", "bsgp_project_df", "bsgp_beta_div",
             "bsgp_beta_div_deriv", "bsgp_beta_div_grad_parts", "bsgp_device_synchronize",
             "bsgp_last_error", "bsgp_abi_version", "bsgp_extract_tiles", "bsgp_coadd_tiles",
             "bsgp_fits_to_f64", "bsgp_psf_stamps", "bsgp_plan_set_psfs"]
@@ -215,12 +217,14 @@ class Plan:
 
     # ------------------------------------------------------------------ solve
     def solve(self, gn, bkg, params, flux=None, x0=None, beta0=None, want_times=True, obj=None,
-              want_iterates=False):
+              want_iterates=False, profile=False):
         """Batched solve on device tensors: gn [B,H,W] f64; bkg [B] or [B,H,W];
         flux/beta0 [B] or None; x0 [B,H,W] or None; obj [B,H,W] or None (then
         "err" holds the per-iteration relative error); want_iterates adds
         "x_iter" [B,MAXIT,H,W].  Asynchronous on the current stream; returns a
-        dict of device output tensors."""
+        dict of device output tensors.  profile=True runs bsgp_solve_profiled
+        (one stream, synchronous) and adds "kernel_ms" / "launches" [5]: setup,
+        k_dir, k_col, k_ls, k_bb."""
         B = gn.shape[0]
         M1 = params.MAXIT + 1
         dev = gn.device
@@ -242,6 +246,14 @@ class Plan:
         outs = Outputs(*[_ptr(out[k]) for k in ["x", "iters", "discr", "times", "crit", "flags",
                                                  "beta_final", "counters", "err", "x_iter"]])
         self._keep = (gn, bkg, flux, x0, beta0, obj)
+        if profile:
+            kms = np.zeros(5, np.float64)
+            nl = np.zeros(5, np.int64)
+            check(lib().bsgp_solve_profiled(self.h, B, ctypes.byref(params), ctypes.byref(ins),
+                                            ctypes.byref(outs), current_stream(),
+                                            kms.ctypes.data, nl.ctypes.data))
+            out["kernel_ms"], out["launches"] = kms, nl
+            return out
         check(lib().bsgp_solve_device(self.h, B, ctypes.byref(params), ctypes.byref(ins),
                                       ctypes.byref(outs), current_stream()))
         return out

@@ -594,8 +594,48 @@ static int check_params(const bsgp_params* q) {
   return BSGP_OK;
 }
 
+// Profiled solves: events around every kernel class of every iteration.
+struct SolveProf {
+  std::vector<hipEvent_t> ev;  // [MAXIT][6] + setup pair
+  double* kernel_ms;
+  int64_t* launches;
+};
+
+static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_inputs* in,
+                      const bsgp_outputs* out, void* stream, SolveProf* prof);
+
 int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_inputs* in,
                       const bsgp_outputs* out, void* stream) {
+  return solve_impl(p, B, prm, in, out, stream, nullptr);
+}
+
+int bsgp_solve_profiled(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_inputs* in,
+                        const bsgp_outputs* out, void* stream, double* kernel_ms,
+                        int64_t* launches) {
+  if (!kernel_ms || !launches) return fail(BSGP_ERR_ARG, "kernel_ms / launches missing");
+  if (!prm) return fail(BSGP_ERR_ARG, "params is NULL");
+  if (!p) return fail(BSGP_ERR_ARG, "plan is NULL");
+  HIP_TRY(hipSetDevice(p->device));
+  SolveProf prof;
+  prof.kernel_ms = kernel_ms;
+  prof.launches = launches;
+  const size_t nev = 6 * (size_t)(prm->MAXIT > 0 ? prm->MAXIT : 0) + 2;
+  prof.ev.resize(nev, nullptr);
+  int rc = BSGP_OK;
+  for (size_t i = 0; i < nev && rc == BSGP_OK; ++i)
+    if (hipEventCreate(&prof.ev[i]) != hipSuccess) rc = fail(BSGP_ERR_HIP, "event create failed");
+  if (rc == BSGP_OK) {
+    bsgp_params q = *prm;
+    q.streams = 1;  // one stream: kernel spans do not overlap
+    rc = solve_impl(p, B, &q, in, out, stream, &prof);
+  }
+  for (hipEvent_t e : prof.ev)
+    if (e) (void)hipEventDestroy(e);
+  return rc;
+}
+
+static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_inputs* in,
+                      const bsgp_outputs* out, void* stream, SolveProf* prof) {
   if (!p) return fail(BSGP_ERR_ARG, "plan is NULL");
   int rc = check_params(prm);
   if (rc) return rc;
@@ -687,16 +727,21 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     sa[j] = a;
     sa[j].img0 = (int)((int64_t)B * j / S);
     sa[j].nimg = (int)((int64_t)B * (j + 1) / S) - sa[j].img0;
+    if (prof) HIP_TRY(hipEventRecord(prof->ev[0], ss[j]));
     HIP_TRY(launch_setup(sa[j], p->lds_bytes, ss[j]));
+    if (prof) HIP_TRY(hipEventRecord(prof->ev[1], ss[j]));
     if (track) HIP_TRY(launch_track(sa[j], 0, ss[j]));
   }
   // Fixed-length runs (stop_criterion 0/1) are launched back to back with no
   // host synchronisation; data-dependent stop rules poll the counter.
   const bool data_stop = prm->stop_criterion >= 2 && prm->stop_criterion <= 4;
   const int poll = data_stop ? (B <= 4 ? 1 : 4) : 0;
+  int it_run = 0;
   for (int it = 1; it <= prm->MAXIT; ++it) {
+    it_run = it;
     for (int j = 0; j < S; ++j) {
-      HIP_TRY(launch_iteration(sa[j], K, p->lds_bytes, ss[j]));
+      HIP_TRY(launch_iteration(sa[j], K, p->lds_bytes, ss[j],
+                               prof ? &prof->ev[2 + 6 * (size_t)(it - 1)] : nullptr));
       if (track) HIP_TRY(launch_track(sa[j], it, ss[j]));
     }
     if (poll && it < prm->MAXIT && it % poll == 0) {
@@ -710,6 +755,28 @@ int bsgp_solve_device(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     for (int j = 0; j < S; ++j) {
       HIP_TRY(hipEventRecord(p->ev_join[j], ss[j]));
       HIP_TRY(hipStreamWaitEvent(s, p->ev_join[j], 0));
+    }
+  }
+  if (prof) {
+    // kernel classes: 0 setup, 1 dir, 2 col (A and AT launches), 3 ls, 4 bb
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int k = 0; k < 5; ++k) {
+      prof->kernel_ms[k] = 0.0;
+      prof->launches[k] = 0;
+    }
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, prof->ev[0], prof->ev[1]));
+    prof->kernel_ms[0] = ms;
+    prof->launches[0] = 1;
+    const int cls[5] = {1, 2, 3, 2, 4};
+    const bool launched[5] = {true, !(sa[0].fuse_col & 5), true, !(sa[0].fuse_col & 2), true};
+    for (int it = 0; it < it_run; ++it) {
+      hipEvent_t* e = &prof->ev[2 + 6 * (size_t)it];
+      for (int k = 0; k < 5; ++k) {
+        HIP_TRY(hipEventElapsedTime(&ms, e[k], e[k + 1]));
+        prof->kernel_ms[cls[k]] += ms;
+        if (launched[k]) prof->launches[cls[k]] += 1;
+      }
     }
   }
   return BSGP_OK;

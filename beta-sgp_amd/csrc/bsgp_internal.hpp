@@ -75,7 +75,9 @@ struct SolveArgs {
 };
 
 hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s);
-hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s);
+// ev: NULL, or 6 events recorded around the kernels of one iteration (profiled solves)
+hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s,
+                            hipEvent_t* ev = nullptr);
 hipError_t launch_track(const SolveArgs& a, int it, hipStream_t s);
 hipError_t launch_build_tf(const Geo& g, const double* kc, cd* spec, cd* tf, double scale,
                            int conj, size_t lds, hipStream_t s);

@@ -1588,10 +1588,16 @@ hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s) {
   return hipGetLastError();
 }
 template <bool COOP>
-static void launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
+static void launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipStream_t s,
+                               hipEvent_t* ev) {
   const dim3 grid(a.nimg * a.T), gcol(a.nimg * a.Tc), block(kBlock);
+  // ev (profiled solves): recorded before k_dir and after every kernel class
+  // (dir, col of A, ls, col of AT, bb); a class not launched gets an empty span
+  if (ev) (void)hipEventRecord(ev[0], s);
   hipLaunchKernelGGL((k_dir<COOP>), grid, block, lds, s, a);
+  if (ev) (void)hipEventRecord(ev[1], s);
   if (!(a.fuse_col & 5)) hipLaunchKernelGGL((k_col<COOP>), gcol, block, lds, s, a, 0);
+  if (ev) (void)hipEventRecord(ev[2], s);
   // line-search kernel specialised on trial width, objective mode, adaptivity
   const bsgp_params& P = a.prm;
   const bool adapt = P.adapt_beta && P.variant == BSGP_VARIANT_BETA;
@@ -1623,14 +1629,17 @@ static void launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipStream_
   } else {
     hipLaunchKernelGGL((k_ls<2, -1, false, COOP>), grid, block, lds, s, a);
   }
+  if (ev) (void)hipEventRecord(ev[3], s);
   if (!(a.fuse_col & 2)) hipLaunchKernelGGL((k_col<COOP>), gcol, block, lds, s, a, 1);
+  if (ev) (void)hipEventRecord(ev[4], s);
   hipLaunchKernelGGL((k_bb<COOP>), grid, block, lds, s, a);
+  if (ev) (void)hipEventRecord(ev[5], s);
 }
-hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s) {
+hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s, hipEvent_t* ev) {
   if (a.g.coop)
-    launch_iteration_t<true>(a, K, lds, s);
+    launch_iteration_t<true>(a, K, lds, s, ev);
   else
-    launch_iteration_t<false>(a, K, lds, s);
+    launch_iteration_t<false>(a, K, lds, s, ev);
   return hipGetLastError();
 }
 hipError_t launch_track(const SolveArgs& a, int it, hipStream_t s) {

@@ -454,7 +454,7 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
                  use_original_SGP_Afunction=True, adapt_beta=False, betaParam=1.005, lr=1e-3,
                  lr_exp_param=0.1, schedule_lr=False, ls_spec=None, ls_series=None,
                  streams=None, team=None, proj_cache=None, gn_compact=None,
-                 device_out=False):
+                 device_out=False, profile=False):
     torch = _B.torch
     per_image = (psf.dim() if torch.is_tensor(psf) else np.ndim(psf)) == 3
     if not per_image:
@@ -490,25 +490,97 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
         plan = _B.per_image_plan(H, W, psf, mode)
     else:
         plan = _B.get_plan(H, W, np.asarray(psf), mode)
-    out = plan.solve(gns, bkgs, prm, flux=fl, x0=x0, beta0=b0)
+    out = plan.solve(gns, bkgs, prm, flux=fl, x0=x0, beta0=b0, profile=profile)
     if device_out:
         return out
+    prof = {k: out.pop(k) for k in ("kernel_ms", "launches") if k in out}
     torch.cuda.current_stream().synchronize()
     _B.check_status(out["counters"])
-    return {k: (v.cpu().numpy() if v is not None else None) for k, v in out.items()}
+    res = {k: (v.cpu().numpy() if v is not None else None) for k, v in out.items()}
+    res.update(prof)
+    return res
 
 
-def sgp_batch(gns, psf, bkgs, **kw):
+def on_devices(devices, n, work):
+    """Shard n independent items over GPUs: contiguous shards [lo, hi), one
+    host thread per device, ``work(device, lo, hi)`` run with that device
+    current (images and beta candidates are independent, so no
+    collective; the C library holds no Python lock while a solve runs).
+    Returns the per-shard results in device order."""
+    import threading
+    devices = list(devices)
+    k = len(devices)
+    if k == 0:
+        raise ValueError("devices is empty")
+    bounds = [(n * j // k, n * (j + 1) // k) for j in range(k)]
+    res, errs = [None] * k, [None] * k
+
+    def run(j):
+        try:
+            with _B.torch.cuda.device(devices[j]):
+                res[j] = work(devices[j], *bounds[j])
+                _B.torch.cuda.current_stream().synchronize()
+        except BaseException as e:  # re-raised in the caller
+            errs[j] = e
+
+    threads = [threading.Thread(target=run, args=(j,)) for j in range(k)
+               if bounds[j][1] > bounds[j][0]]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    for e in errs:
+        if e is not None:
+            raise e
+    return [r for r, (lo, hi) in zip(res, bounds) if hi > lo]
+
+
+def _shard(v, lo, hi, Bn):
+    """The [lo, hi) part of a per-image argument (scalars and shared maps pass)."""
+    if v is None:
+        return None
+    shape = tuple(v.shape) if hasattr(v, "shape") else np.shape(v)
+    if len(shape) in (1, 3) and shape[0] == Bn and Bn > 1:  # [B] values or [B, H, W] maps
+        return v[lo:hi]
+    return v
+
+
+def _solve_sharded(variant, gns, psf, bkgs, devices, betaParams=None, flux=None, **kw):
+    Bn = gns.shape[0]
+    if kw.get("device_out"):
+        raise ValueError("devices=... returns host arrays (device_out is per device)")
+    per_image_psf = (psf.dim() if _B.torch.is_tensor(psf) else np.ndim(psf)) == 3
+
+    def work(dev, lo, hi):
+        return _solve_batch(variant, gns[lo:hi], psf[lo:hi] if per_image_psf else psf,
+                            _shard(bkgs, lo, hi, Bn),
+                            betaParams=_shard(betaParams, lo, hi, Bn),
+                            flux=_shard(flux, lo, hi, Bn), **kw)
+
+    parts = on_devices(devices, Bn, work)
+    return {k: (np.concatenate([p[k] for p in parts]) if parts[0][k] is not None else None)
+            for k in parts[0]}
+
+
+def sgp_batch(gns, psf, bkgs, devices=None, **kw):
     """KL-SGP on a batch [B, H, W] (one launch); psf is one [kh, kw] PSF or
     [B, kh, kw] (a PSF per image).  Returns a dict of arrays:
-    x [B,H,W], iters [B], discr [B,MAXIT+1], times, crit, flags, counters."""
+    x [B,H,W], iters [B], discr [B,MAXIT+1], times, crit, flags, counters.
+    ``devices=[0, 1, ...]`` shards the batch over those GPUs (contiguous
+    shards, one host thread per GPU, results concatenated in batch order)."""
+    if devices is not None:
+        return _solve_sharded(_B.BSGP_VARIANT_KL, gns, psf, bkgs, devices, **kw)
     return _solve_batch(_B.BSGP_VARIANT_KL, gns, psf, bkgs, **kw)
 
 
-def sgp_betaDiv_batch(gns, psf, bkgs, betaParams=None, **kw):
+def sgp_betaDiv_batch(gns, psf, bkgs, betaParams=None, devices=None, **kw):
     """beta-SGP on a batch [B, H, W] with per-image initial betaParam (the
     multi-start beta search of application_sgp_subdivisions.py:70-107 as one
-    launch).  Returns the dict of :func:`sgp_batch` plus beta_final [B]."""
+    launch).  Returns the dict of :func:`sgp_batch` plus beta_final [B].
+    ``devices`` shards (image, beta) pairs over GPUs as in :func:`sgp_batch`."""
+    if devices is not None:
+        return _solve_sharded(_B.BSGP_VARIANT_BETA, gns, psf, bkgs, devices,
+                              betaParams=betaParams, **kw)
     return _solve_batch(_B.BSGP_VARIANT_BETA, gns, psf, bkgs, betaParams=betaParams, **kw)
 
 
@@ -526,7 +598,8 @@ def app_beta_candidates(seeds=APP_BETA_SEEDS, loc=1.0, scale=0.05):
     return out
 
 
-def sgp_betaDiv_multistart(gn, psf, bkg, betas=None, score=None, final_solve=True, **kwargs):
+def sgp_betaDiv_multistart(gn, psf, bkg, betas=None, score=None, final_solve=True, devices=None,
+                           **kwargs):
     """The beta search of application_sgp_subdivisions.py:69-107 as two
     launches: every candidate initial beta (default: the application's five
     seeds) is solved in ONE batched launch, the host takes the argmin of
@@ -538,7 +611,8 @@ def sgp_betaDiv_multistart(gn, psf, bkg, betas=None, score=None, final_solve=Tru
     needs photutils, which this package does not carry, so the caller passes
     it.  Without one the candidates are ranked by their final discrepancy
     discr[-1] (a stand-in, not the application's choice).  ``kwargs`` are
-    sgp_betaDiv's keyword arguments.
+    sgp_betaDiv's keyword arguments.  ``devices=[...]`` spreads the
+    candidates over GPUs (one batched launch per GPU).
 
     Returns (x, iters, discr, times, None) of the final solve and a dict with
     "betas", "scores", "best_beta" and "candidates" (each candidate's
@@ -559,13 +633,19 @@ def sgp_betaDiv_multistart(gn, psf, bkg, betas=None, score=None, final_solve=Tru
     args.update(kw)
     if args["save"]:
         raise ValueError("save=True writes one set of files per solve: use sgp_betaDiv")
-    runs = _run(_B.BSGP_VARIANT_BETA, gn, psf, bkg, args["init_recon"], args["proj_type"],
-                args["stop_criterion"], args["MAXIT"], args["gamma"], args["beta"],
-                args["alpha"], args["alpha_min"], args["alpha_max"], args["M_alpha"],
-                args["tau"], args["M"], args["max_projs"], False, None, args["verbose"],
-                args["flux"], args["ccd_sat_level"], args["scale_data"], False,
-                args["tol_convergence"], args["use_original_SGP_Afunction"],
-                dict(bkw, betaParam=betas[0]), betas=betas)
+    def work(dev, lo, hi):
+        return _run(_B.BSGP_VARIANT_BETA, gn, psf, bkg, args["init_recon"], args["proj_type"],
+                    args["stop_criterion"], args["MAXIT"], args["gamma"], args["beta"],
+                    args["alpha"], args["alpha_min"], args["alpha_max"], args["M_alpha"],
+                    args["tau"], args["M"], args["max_projs"], False, None, args["verbose"],
+                    args["flux"], args["ccd_sat_level"], args["scale_data"], False,
+                    args["tol_convergence"], args["use_original_SGP_Afunction"],
+                    dict(bkw, betaParam=betas[lo]), betas=betas[lo:hi])
+
+    if devices is None:
+        runs = work(None, 0, len(betas))
+    else:
+        runs = [r for part in on_devices(devices, len(betas), work) for r in part]
     cands = [(x, it, d, t, None) for x, it, d, t, _ in runs]
     scores = [float(score(c[0])) if score is not None else float(c[2][-1]) for c in cands]
     best = int(np.argmin(scores))

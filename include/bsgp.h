@@ -156,6 +156,15 @@ int bsgp_plan_info(bsgp_plan plan, int32_t* P, int32_t* Q, int64_t* slot_bytes,
 int bsgp_solve_device(bsgp_plan plan, int32_t B, const bsgp_params* params,
                       const bsgp_inputs* in, const bsgp_outputs* out, void* stream);
 
+/* Measurement: bsgp_solve_device on the one stream `stream` (params->streams is
+ * taken as 1) with a HIP event recorded around every kernel launch;
+ * kernel_ms[k] and launches[k] (k < 5) receive the summed span and the launch
+ * count of kernel class k: 0 setup, 1 k_dir, 2 k_col (A and AT), 3 k_ls, 4 k_bb.
+ * Synchronous (waits for the solve). */
+int bsgp_solve_profiled(bsgp_plan plan, int32_t B, const bsgp_params* params,
+                        const bsgp_inputs* in, const bsgp_outputs* out, void* stream,
+                        double* kernel_ms, int64_t* launches);
+
 /* Same with host buffers (copies in, solves, copies out). Synchronous. */
 int bsgp_solve_host(bsgp_plan plan, int32_t B, const bsgp_params* params,
                     const bsgp_inputs* in, const bsgp_outputs* out);

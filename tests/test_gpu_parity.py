@@ -376,3 +376,37 @@ def test_gn_compact_is_bitwise_neutral(sgpmod):
         b = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, team=team, gn_compact=0, **kw)
         np.testing.assert_array_equal(a["x"], b["x"])
         np.testing.assert_array_equal(a["discr"], b["discr"])
+
+
+# ------------------------------------------------------------ multi-device API
+def test_devices_sharding_is_bitwise_equal(sgpmod):
+    """devices=[...] shards (image, beta) pairs over GPUs, one host thread per
+    device.  On a one-GPU box: devices=[0] and devices=[0, 0]
+    (two threads, two shards on the same GPU) give the plain batch's bits."""
+    fx = golden("ref_lin64_beta.npz")
+    gn = fx["gn"].astype(np.float64)
+    gns = np.stack([np.roll(gn, 5 * i, 1) for i in range(6)])
+    betas = [1.05, 0.97, 1.02, 0.99, 1.08, 1.01]
+    kw = dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=10, alpha=10.0,
+              ccd_sat_level=65000.0, use_original_SGP_Afunction=False, schedule_lr=True,
+              adapt_beta=False, team=1)
+    plain = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, betaParams=betas, **kw)
+    for devs in ([0], [0, 0]):
+        sh = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, betaParams=betas, devices=devs, **kw)
+        for key in ("x", "iters", "discr", "beta_final"):
+            np.testing.assert_array_equal(sh[key], plain[key])
+
+
+def test_profiled_solve_reports_every_kernel_class(sgpmod):
+    """bsgp_solve_profiled (bench.py's per-kernel roofline): same results as a
+    plain one-stream solve, and one launch of k_dir / k_ls / k_bb per
+    iteration with positive spans."""
+    fx = golden("ref_lin256_beta.npz")
+    kw = ref_kwargs(fx)
+    gns = np.stack([fx["gn"].astype(np.float64)] * 8)
+    a = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, team=1, streams=1, **kw)
+    b = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, team=1, profile=True, **kw)
+    np.testing.assert_array_equal(a["x"], b["x"])
+    it = int(kw["MAXIT"])
+    assert list(b["launches"]) == [1, it, it, it, it]  # setup, dir, col (A), ls (+AT), bb
+    assert np.all(b["kernel_ms"] > 0)

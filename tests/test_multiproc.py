@@ -48,3 +48,36 @@ def test_two_rank_aggregation_gloo():
         assert t == 2.0                       # max over ranks
         assert n == 100 * 1024 * 3            # summed work of both ranks
     assert res[0][4] < res[1][3]              # disjoint shards
+
+
+def test_bench_spawns_one_rank_per_gpu_stub():
+    """`bench.py --gpus 2` without torchrun starts two rank processes itself
+    (gloo harness, no GPU in --stub mode, a fixed wait per solve): n_gpus is
+    the number of ranks that ran, C5's 8192 images are split 4096 + 4096, and
+    value counts the image-iterations of both ranks."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--stub",
+                          "--steps", "3", "--warmup", "1", "--no-cpu", "--config", "c5",
+                          "--maxit", "10"], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["scaling"] == "strong"
+    assert r["config"]["images_per_gpu"] == 4096 and r["config"]["images_total"] == 8192
+    # 2 ranks x 4096 images x 10 iterations per step; >= 10 ms wait per step
+    assert r["value"] <= 2 * 4096 * 10 / 0.010 * 1.001
+    assert r["value"] == pytest.approx(3 * 2 * 4096 * 10 / (r["ms_per_step"] * 3 / 1e3), rel=1e-9)
+
+
+def test_shard_bounds_cover_the_job():
+    import bench
+    for world in (1, 2, 3, 8):
+        parts = [bench.shard_bounds(8192, world, r) for r in range(world)]
+        assert parts[0][0] == 0 and parts[-1][1] == 8192
+        assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
