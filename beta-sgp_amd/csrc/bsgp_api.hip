@@ -485,7 +485,7 @@ int bsgp_plan_destroy(bsgp_plan p) {
   if (p->tw) (void)hipFree(p->tw);
   if (p->tf) (void)hipFree(p->tf);
   if (p->ws) (void)hipFree(p->ws);
-  for (int i = 0; i < p->nsub; ++i) {
+  for (int i = 1; i < p->nsub; ++i) {
     if (p->sub[i]) (void)hipStreamDestroy(p->sub[i]);
     if (p->ev_join[i]) (void)hipEventDestroy(p->ev_join[i]);
   }
@@ -684,6 +684,9 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   a.plist_stride = 0;
   a.lcap = 0;
   a.pw = p->pw;
+  a.ls_cap = (prm->beta > 0.0 && prm->beta < 1.0)
+                 ? (int)std::ceil(std::log(1e-12) / std::log(prm->beta)) + 2
+                 : 4096;
   if (prm->proj_cache && prm->proj_type == 1) {
     a.lcap = proj_list_cap(p->g, T);
     const size_t half = round_up((size_t)a.lcap * T * kBlock, 32);
@@ -702,9 +705,12 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   int S = prm->streams < 1 ? 1 : prm->streams;
   if (S > bsgp_plan_s::kMaxStreams) S = bsgp_plan_s::kMaxStreams;
   if (S > B) S = B;
+  // sub-batch 0 runs on the caller's stream itself, sub-batches 1..S-1 on the
+  // plan's streams: S streams in all, so S = 4 fits the 4 hardware queues HIP
+  // opens per process (GPU_MAX_HW_QUEUES)
   if (S > 1 && p->nsub < S) {
     if (!p->ev_fork) HIP_TRY(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
-    for (int i = p->nsub; i < S; ++i) {
+    for (int i = (p->nsub > 1 ? p->nsub : 1); i < S; ++i) {
       HIP_TRY(hipStreamCreateWithFlags(&p->sub[i], hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&p->ev_join[i], hipEventDisableTiming));
     }
@@ -722,8 +728,8 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   const bool track = out->err != nullptr || out->x_iter != nullptr;
   if (S > 1) HIP_TRY(hipEventRecord(p->ev_fork, s));
   for (int j = 0; j < S; ++j) {
-    ss[j] = S > 1 ? p->sub[j] : s;
-    if (S > 1) HIP_TRY(hipStreamWaitEvent(ss[j], p->ev_fork, 0));
+    ss[j] = j > 0 ? p->sub[j] : s;
+    if (j > 0) HIP_TRY(hipStreamWaitEvent(ss[j], p->ev_fork, 0));
     sa[j] = a;
     sa[j].img0 = (int)((int64_t)B * j / S);
     sa[j].nimg = (int)((int64_t)B * (j + 1) / S) - sa[j].img0;
@@ -752,7 +758,7 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     }
   }
   if (S > 1) {
-    for (int j = 0; j < S; ++j) {
+    for (int j = 1; j < S; ++j) {
       HIP_TRY(hipEventRecord(p->ev_join[j], ss[j]));
       HIP_TRY(hipStreamWaitEvent(s, p->ev_join[j], 0));
     }

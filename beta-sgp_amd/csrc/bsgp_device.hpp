@@ -830,6 +830,11 @@ __device__ __forceinline__ void row_inv_fwd(const Geo& G, const Part& D, cd* spe
   }
 }
 
+// measured on C3 (A/B): the TF loaded after the forward FFT keeps k_col at
+// 111 VGPRs (4 waves/SIMD) and runs 8 % faster than batching it with the column
+#ifndef BSGP_COL_TFPRE
+#define BSGP_COL_TFPRE false
+#endif
 // col_conv: every wave owns whole columns: it streams stored column k
 // (contiguous, H rows) into its LDS buffer, zero-fills rows H..P-1, runs the
 // forward P-point FFT, multiplies by tf[k][:], runs the inverse FFT and
@@ -845,7 +850,9 @@ __device__ __forceinline__ void col_conv(const Geo& G, const Part& D, cd* spec, 
   if (w < G.nfw) {
     cd* a = lds + w * 2 * G.lpad;
     cd* b = a + G.lpad;
-    const bool one = G.P <= 64 * kPCH;  // column and TF loads in one batch
+    // column and TF loads in one batch before the forward FFT (the TF stays
+    // in registers across it), or the TF loaded after the FFT
+    const bool one = BSGP_COL_TFPRE && G.P <= 64 * kPCH;
     for (int k = D.gw0 + w; k < G.Qh; k += D.gws) {
       cd* col = spec + (size_t)k * G.H;
       const cd* t = tf + (size_t)k * G.P;

@@ -72,6 +72,8 @@ struct SolveArgs {
   size_t plist_stride;  // doubles per image (both arrays)
   int lcap;             // list capacity per thread (pixels one thread streams)
   PwProg pw;            // numpy float32 sum order over N (params.gn_f32)
+  int ls_cap;           // line-search trial cap: lam = beta^(k-1) < 1e-12 ends the search
+                        // (sgp.py:336) by trial ceil(log 1e-12 / log beta) + 1 for 0 < beta < 1
 };
 
 hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s);

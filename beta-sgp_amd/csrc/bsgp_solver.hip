@@ -66,7 +66,7 @@ namespace bsgp {
 #define BSGP_BB_PRE false
 #endif
 #ifndef BSGP_BB_JCH
-#define BSGP_BB_JCH 2
+#define BSGP_BB_JCH 1  // one column per operand batch: 117 VGPRs, 4 waves/SIMD (k_bb -17 %, A/B)
 #endif
 
 // Phase profile (builds with -DBSGP_PHASE_PROF only): thread 0 of every
@@ -903,11 +903,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   };
   double fr = st.Fold[0];
   for (int k = 1; k < P.M; ++k) fr = py_max2(fr, st.Fold[k]);
-  // lam = beta^(k-1) at trial k; lam < 1e-12 forces acceptance (sgp.py:336),
-  // so for 0 < beta < 1 the cap below is never reached
-  const int ls_cap = (P.beta > 0.0 && P.beta < 1.0)
-                         ? (int)ceil(log(1e-12) / log(P.beta)) + 2
-                         : 4096;
+  const int ls_cap = A.ls_cap;  // trial cap (bsgp_api.hip): never reached for 0 < beta < 1
   Objective obj = make_obj(A, st.beta);
   double lam = 1.0;
   double f_acc = 0.0;
@@ -926,7 +922,10 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   constexpr int MS = 6;
   constexpr double kSeriesRho = 0.01;
   const bool series = (MODE == 3 || MODE == 4) && !adapt && P.ls_series != 0;
-  double Pm[MS + 1], Qm[MS + 1];
+  // the moments and binomial coefficients are the same in every thread: they
+  // live in LDS after the first pass (ser[0..3][MS+1] = P, Q, binom(b, m),
+  // binom(b-1, m)), not in VGPRs across the trial passes
+  double* ser = red + kWaves * kMaxRed + kMaxRed + 8;
   double rho = INFINITY;
   // ---- pass 1, fused into the inverse rows that produce d_tf: lam = 1 direct
   {
@@ -981,10 +980,11 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
     team_sum<N1>(t1, red, tm);
     if (series) rho = team_max(umax, red, tm);
     PH_ADD(4, tk0);
-#pragma unroll
-    for (int m = 0; m <= MS; ++m) {
-      Pm[m] = t1[4 + m];
-      Qm[m] = t1[4 + MS + 1 + m];
+    if (series && threadIdx.x == 0) {
+      for (int m = 0; m <= MS; ++m) {
+        ser[m] = t1[4 + m];
+        ser[MS + 1 + m] = t1[4 + MS + 1 + m];
+      }
     }
     if (adapt) konst = t1[2];
     ++passes;
@@ -1002,25 +1002,26 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
     }
   }
   // binomial coefficients of the series
-  double cb[MS + 1], cb1[MS + 1];
-  if (series) {
-    cb[0] = 1.0;
-    cb1[0] = 1.0;
-#pragma unroll
+  if (series && threadIdx.x == 0) {
+    double c0 = 1.0, c1 = 1.0;
+    ser[2 * (MS + 1)] = 1.0;
+    ser[3 * (MS + 1)] = 1.0;
     for (int m = 1; m <= MS; ++m) {
-      cb[m] = cb[m - 1] * (obj.beta - (m - 1)) / m;
-      cb1[m] = cb1[m - 1] * (obj.beta - 1 - (m - 1)) / m;
+      c0 = c0 * (obj.beta - (m - 1)) / m;
+      c1 = c1 * (obj.beta - 1 - (m - 1)) / m;
+      ser[2 * (MS + 1) + m] = c0;
+      ser[3 * (MS + 1) + m] = c1;
     }
   }
+  __syncthreads();
   PH_T(tk1);
   while (!accepted) {
     if (series && lam * rho <= kSeriesRho) {
       // closed-form trial: no pass over the image
       double s0 = 0.0, s1 = 0.0, lm = 1.0;
-#pragma unroll
       for (int m = 0; m <= MS; ++m) {
-        s0 += cb[m] * lm * Pm[m];
-        s1 += cb1[m] * lm * Qm[m];
+        s0 += ser[2 * (MS + 1) + m] * lm * ser[m];
+        s1 += ser[3 * (MS + 1) + m] * lm * ser[MS + 1 + m];
         lm *= lam;
       }
       const double fk =

@@ -56,7 +56,7 @@ DEFAULT_COLUMNS = ['label', 'xcentroid', 'ycentroid', 'sky_centroid',
 
 LS_SPEC_DEFAULT = 2  # line-search trial lambdas evaluated per pass over the data
 LS_SERIES_DEFAULT = 1  # small line-search steps from the moment series (general beta)
-STREAMS_DEFAULT = 3  # sub-batch streams of a batched solve (+ the caller's = 4 HW queues; 4 sub-streams collapse under the default GPU_MAX_HW_QUEUES=4)
+STREAMS_DEFAULT = 4  # sub-batches of a batched solve: the caller's stream + 3 plan streams = the 4 HW queues HIP opens (C3 A/B: 4 > 3 > 2)
 TEAM_DEFAULT = 0  # workgroups per image: 0 = auto (spread small batches over the CUs)
 PROJ_CACHE_DEFAULT = 1  # projectDF evaluations inside a known root bracket read a pixel list
 GN_COMPACT_DEFAULT = 1  # f32-exact observed images stored in f32 (bit-identical results)

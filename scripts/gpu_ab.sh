@@ -20,6 +20,12 @@ python - "$TAG" "$REPS" "${SPECS[@]}" <<'PY'
 import json, sys, statistics
 tag, reps, specs = sys.argv[1], int(sys.argv[2]), sys.argv[3:]
 for k, v in enumerate(specs):
-    vals = [json.load(open(f"gpurun_out/{tag}_{k}_{i}.json"))["value"] for i in range(reps)]
-    print(f"{v:28s} median {statistics.median(vals):9.0f}  all {[round(x) for x in vals]}")
+    js = [json.load(open(f"gpurun_out/{tag}_{k}_{i}.json")) for i in range(reps)]
+    vals = [j["value"] for j in js]
+    kern = ""
+    rl = js[-1].get("roofline")
+    if rl and "kernels" in rl:
+        kern = " ".join(f"{n}={d.get('ms_per_launch', d['ms_total']):.3f}"
+                        for n, d in rl["kernels"].items())
+    print(f"{v:28s} median {statistics.median(vals):9.0f}  all {[round(x) for x in vals]}  {kern}")
 PY
