@@ -111,7 +111,8 @@ def synth_batch(B, n, k, nstars, seed0, bkg=100.0, circular=False):
     return gn.contiguous(), psf
 
 
-def solve_kwargs(maxit, ls_spec, streams=None, team=None, circular=False, proj_cache=None):
+def solve_kwargs(maxit, ls_spec, streams=None, team=None, circular=False, proj_cache=None,
+                 storage="f64"):
     max_projs, gamma, beta, alpha_min, alpha_max, alpha, M_alpha, tau, M = (
         1000, 1e-4, 0.4, 1e-5, 1e5, 1e1, 3, 0.5, 1)  # sgp.DEFAULT_PARAMS (sgp.py:34)
     return dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=maxit, gamma=gamma, beta=beta,
@@ -119,7 +120,7 @@ def solve_kwargs(maxit, ls_spec, streams=None, team=None, circular=False, proj_c
                 M=M, max_projs=max_projs, ccd_sat_level=65000.0, scale_data=True,
                 use_original_SGP_Afunction=circular, adapt_beta=False, betaParam=1.05, lr=1e-3,
                 lr_exp_param=0.1, schedule_lr=True, ls_spec=ls_spec, streams=streams,
-                team=team, proj_cache=proj_cache)
+                team=team, proj_cache=proj_cache, storage=storage)
 
 
 def cpu_model():
@@ -138,7 +139,7 @@ def cpu_baseline(n, k, nstars, images, maxit, workers, circular=False):
     wall time of the solve phase (pool already warm, inputs built in-task)."""
     import cpu_bench
     kw = solve_kwargs(maxit, None, circular=circular)
-    for key in ("ls_spec", "team", "streams", "proj_cache"):
+    for key in ("ls_spec", "team", "streams", "proj_cache", "storage"):
         kw.pop(key)
     iters, wall, cpu_s = cpu_bench.run_pool(n, k, nstars, images, kw, workers)
     ncpu = os.cpu_count() or 1
@@ -198,11 +199,14 @@ def launch_ranks(n, argv):
     return bad[0] if bad else 0
 
 
-def kernel_bytes(H, W, P, Qh, counters, iters, beta, series, compact, bmap, fused_at_col):
+def kernel_bytes(H, W, P, Qh, counters, iters, beta, series, compact, bmap, fused_at_col,
+                 vb=8.0):
     """Algorithmic HBM bytes of each kernel class over one solve: the passes
     each kernel makes over the per-image vectors (counted on the device) plus
-    its spectrum traffic.  N = H*W pixels; S = 16*H*Qh bytes of
-    stored half spectrum; TF = 16*P*Qh bytes of transfer function.
+    its spectrum traffic.  N = H*W pixels; vb = bytes of a
+    stored iterate element (8, or 4 for float32 storage); gn is 4 B when kept
+    compact; S = 16*H*Qh bytes of stored half spectrum; TF = 16*P*Qh bytes of
+    transfer function.
       k_dir: (x, g) per projection pass + 16 B per list entry read; (x, g)
              for the direction and its row transforms; writes the spectrum.
       k_col: reads and writes the spectrum, reads the TF (A; AT too if unfused).
@@ -219,13 +223,13 @@ def kernel_bytes(H, W, P, Qh, counters, iters, beta, series, compact, bmap, fuse
     proj_passes, list_reads = float(np.sum(counters[:, 6])), float(np.sum(counters[:, 7]))
     ls_passes = float(np.sum(counters[:, 2]))
     b = {}
-    b["k_dir"] = 16.0 * N * proj_passes + 16.0 * list_reads + it * (16.0 * N + S)
+    b["k_dir"] = 2.0 * vb * N * proj_passes + 16.0 * list_reads + it * (2.0 * vb * N + S)
     col_per = 2.0 * S + TF
-    b["k_ls"] = (it * (S + N * (8.0 + gb + (8.0 if series else 0.0) + bb) + 8.0 * N)
-                 + (ls_passes - it) * N * (16.0 + gb + bb)
-                 + it * (N * (16.0 + gb + bb) + N * (16.0 if beta else 8.0) + S)
+    b["k_ls"] = (it * (S + N * (vb + gb + (vb if series else 0.0) + bb) + vb * N)
+                 + (ls_passes - it) * N * (2.0 * vb + gb + bb)
+                 + it * (N * (2.0 * vb + gb + bb) + N * (2.0 * vb if beta else vb) + S)
                  + (it * col_per if fused_at_col else 0.0))
-    b["k_bb"] = it * (S + N * ((8.0 if beta else 0.0) + 16.0) + 16.0 * N)
+    b["k_bb"] = it * (S + N * ((vb if beta else 0.0) + 2.0 * vb) + 2.0 * vb * N)
     b["k_col"] = it * col_per * (1.0 if fused_at_col else 2.0)
     return b
 
@@ -293,7 +297,7 @@ def main():
         B = args.batch if args.batch else cfg["batch"]
         seed0 = shard_seed0(rank, B)
     kw = solve_kwargs(args.maxit, args.ls_spec, args.streams, args.team, circular=circ,
-                      proj_cache=args.proj_cache)
+                      proj_cache=args.proj_cache, storage=args.storage)
 
     if args.stub:
         def step():
@@ -362,7 +366,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": "f64" if args.storage == "f64" else "f32 storage, f64 arithmetic",
         "data": "synthetic (SURVEY §8d generator: pareto point sources * 25x25 Gaussian PSF "
                 "+ Poisson, bkg 100), built on device",
         "config": {"workload": workload, "images_per_gpu": B,
@@ -404,12 +408,12 @@ def roofline(args, kw, gn, psf, bkg, B, n, solve_ms):
     import sgp
     prof = sgp.sgp_betaDiv_batch(gn, psf, bkg, profile=True, **kw)
     plan = _bsgp.get_plan(n, n, psf, _bsgp.BSGP_CONV_CIRCULAR if kw["use_original_SGP_Afunction"]
-                          else _bsgp.BSGP_CONV_LINEAR_FILL)
+                          else _bsgp.BSGP_CONV_LINEAR_FILL, storage=kw["storage"])
     cnt, iters = prof["counters"], prof["iters"]
     team = int(cnt[0, 5])
     kb = kernel_bytes(n, n, plan.P, plan.Q // 2 + 1, cnt, iters, beta=True, series=True,
                       compact=sgp.GN_COMPACT_DEFAULT == 1, bmap=False,
-                      fused_at_col=(team == 1))
+                      fused_at_col=(team == 1), vb=4.0 if kw["storage"] == "f32" else 8.0)
     names = ["k_setup", "k_dir", "k_col", "k_ls", "k_bb"]
     ms, nl = prof["kernel_ms"], prof["launches"]
     kernels = {}

@@ -282,30 +282,43 @@ _plan_cache = {}
 _plan_cache_lock = threading.Lock()
 
 
-def get_plan(H, W, psf, conv_mode):
-    """Plans are cached per (shape, psf bytes, mode, device, host thread): a
-    plan's workspace belongs to one solve at a time (include/bsgp.h: one plan
-    per device per host thread), so threads never share one."""
+STORAGE = {"f64": BSGP_STORAGE_F64, "f32": BSGP_STORAGE_F32}
+
+
+def storage_code(storage):
+    """'f64' / 'f32' (or the BSGP_STORAGE_* value) -> BSGP_STORAGE_*."""
+    if storage in STORAGE.values():
+        return storage
+    if storage not in STORAGE:
+        raise ValueError(f"storage must be 'f64' or 'f32', not {storage!r}")
+    return STORAGE[storage]
+
+
+def get_plan(H, W, psf, conv_mode, storage="f64"):
+    """Plans are cached per (shape, psf bytes, mode, storage, device, host
+    thread): a plan's workspace belongs to one solve at a time (include/bsgp.h:
+    one plan per device per host thread), so threads never share one."""
     require_gpu()
     psf = np.ascontiguousarray(psf, dtype="<f8")
     dev = torch.cuda.current_device()
-    key = (H, W, psf.shape, psf.tobytes(), conv_mode, dev, threading.get_ident())
+    st = storage_code(storage)
+    key = (H, W, psf.shape, psf.tobytes(), conv_mode, st, dev, threading.get_ident())
     with _plan_cache_lock:
         p = _plan_cache.get(key)
         if p is None:
             if len(_plan_cache) > 16:
                 _plan_cache.clear()
-            p = Plan(H, W, psf, conv_mode, dev)
+            p = Plan(H, W, psf, conv_mode, dev, storage=st)
             _plan_cache[key] = p
     return p
 
 
-def per_image_plan(H, W, psfs, conv_mode):
+def per_image_plan(H, W, psfs, conv_mode, storage="f64"):
     """A plan whose image i uses psfs[i] ([B, kh, kw], numpy or CUDA tensor);
     not cached (it holds B transfer-function pairs)."""
     require_gpu()
     dev = psfs.to(dtype=torch.float64).contiguous() if torch.is_tensor(psfs) else to_dev(psfs)
-    p = Plan(H, W, dev[0].cpu().numpy(), conv_mode)
+    p = Plan(H, W, dev[0].cpu().numpy(), conv_mode, storage=storage_code(storage))
     return p.set_psfs(dev)
 
 

@@ -130,6 +130,7 @@ struct bsgp_plan_s {
   size_t ws_slots = 0;
   size_t slot_stride = 0;
   size_t vec_stride = 0;
+  size_t spec_off = 0;
   ImgState* st = nullptr;
   size_t st_n = 0;
   int* active = nullptr;     // device counter of images still iterating
@@ -454,12 +455,12 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   }
   const size_t N = (size_t)H * W;
   p->storage = storage;
-  if (storage == BSGP_STORAGE_F32) {
-    bsgp_plan_destroy(p);
-    return fail(BSGP_ERR_UNSUPPORTED, "float32 storage is not built yet");
-  }
+  // slot: gn and bkg in float64 (vec_stride each), the seven iteration vectors
+  // in the storage type, then the half spectrum (complex float64)
   p->vec_stride = round_up(N, 32);
-  p->slot_stride = 9 * p->vec_stride + round_up((size_t)H * g.Qh * 2, 32);
+  const size_t vbytes = storage == BSGP_STORAGE_F32 ? sizeof(float) : sizeof(double);
+  p->spec_off = 2 * p->vec_stride + 7 * p->vec_stride * vbytes / sizeof(double);
+  p->slot_stride = p->spec_off + round_up((size_t)H * g.Qh * 2, 32);
   {
     const std::vector<int> prog = pairwise_program((long)N, &p->pw);
     if (hipMalloc(&p->pwprog, prog.size() * sizeof(int)) != hipSuccess ||
@@ -684,6 +685,8 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   a.plist_stride = 0;
   a.lcap = 0;
   a.pw = p->pw;
+  a.storage = p->storage;
+  a.spec_off = p->spec_off;
   a.ls_cap = (prm->beta > 0.0 && prm->beta < 1.0)
                  ? (int)std::ceil(std::log(1e-12) / std::log(prm->beta)) + 2
                  : 4096;

@@ -72,6 +72,8 @@ struct SolveArgs {
   size_t plist_stride;  // doubles per image (both arrays)
   int lcap;             // list capacity per thread (pixels one thread streams)
   PwProg pw;            // numpy float32 sum order over N (params.gn_f32)
+  int storage;          // BSGP_STORAGE_F64 / F32 (iteration vectors, Bufs<V>)
+  size_t spec_off;      // doubles from a slot's start to its spectrum
   int ls_cap;           // line-search trial cap: lam = beta^(k-1) < 1e-12 ends the search
                         // (sgp.py:336) by trial ceil(log 1e-12 / log beta) + 1 for 0 < beta < 1
 };

@@ -1,88 +1,19 @@
-// bsgp_solver.hip — the persistent batched beta-SGP solve kernel for gfx950
-// and the small standalone kernels behind include/bsgp.h.
+// bsgp_solver.hip — the float64-storage builds of the batched beta-SGP phase
+// kernels (bsgp_kernels.hpp), the standalone kernels behind include/bsgp.h
+// (transfer functions, A/AT, projectDF, betaDiv family) and the dispatch of
+// both storage builds.
 //
 // Reference hot path: restoration/sgp.py:41-438 (sgp, KL) and :506-895
 // (sgp_betaDiv), restoration/flux_conserve_proj.py:7-144 (projectDF).
-//
-// One workgroup = one image in every phase kernel: setup, then per SGP
-// iteration k_dir (projection + direction + rows of d), k_col (columns with
-// A's transfer function), k_ls (line search + accept + rows of w), k_col (AT),
-// k_bb (gradient, x update, Barzilai-Borwein, stop rules).  All scalar
-// control runs on the device; per-image state lives in ImgState.
 #include <hip/hip_runtime.h>
 
-#include "bsgp_device.hpp"
-#include "bsgp_internal.hpp"
+#include <type_traits>
+#include <vector>
+
+#include "bsgp_kernels.hpp"
 
 namespace bsgp {
 
-// The phase kernels are sized for 4 waves per SIMD (<= 128 VGPRs): four
-// 256-thread workgroups = four images per CU, so a 1024-image batch is
-// resident in one round on 256 CUs.
-#ifndef BSGP_OCC4
-#define BSGP_OCC4 __attribute__((amdgpu_waves_per_eu(4, 8)))
-#endif
-
-// Operand batching of the inverse row passes (tuning knobs, see row_inv2)
-#ifndef BSGP_LS1_PRE
-#define BSGP_LS1_PRE false
-#endif
-#ifndef BSGP_LS1_JCH
-#define BSGP_LS1_JCH 1
-#endif
-#ifndef BSGP_DIR_ATTR
-#define BSGP_DIR_ATTR
-#endif
-#ifndef BSGP_COL_ATTR
-#define BSGP_COL_ATTR
-#endif
-// k_ls at 3 waves/SIMD (<= 168 VGPRs; a few spills) with single-column operand
-// batches and plain radix stages in its row passes: +3 % end to end on C3
-// against 2 waves at 216 VGPRs (measured A/B).  Cooperative builds keep 1.
-#ifndef BSGP_LS_ATTR
-#define BSGP_LS_ATTR __attribute__((amdgpu_waves_per_eu(COOP ? 1 : (K <= 2 ? 3 : 2))))
-#endif
-#ifndef BSGP_PROJ_U
-#define BSGP_PROJ_U 4
-#endif
-#ifndef BSGP_DIR_JCH
-#define BSGP_DIR_JCH 4
-#endif
-#ifndef BSGP_DIR_PF
-#define BSGP_DIR_PF true
-#endif
-// composite radix-6/9 FFT stages per row pass (the column pass always uses them):
-// fewer LDS round trips vs ~20 more live VGPRs
-#ifndef BSGP_DIR_COMP
-#define BSGP_DIR_COMP true
-#endif
-#ifndef BSGP_LS_COMP
-#define BSGP_LS_COMP false
-#endif
-#ifndef BSGP_BB_COMP
-#define BSGP_BB_COMP false
-#endif
-#ifndef BSGP_BB_PRE
-#define BSGP_BB_PRE false
-#endif
-#ifndef BSGP_BB_JCH
-#define BSGP_BB_JCH 1  // one column per operand batch: 117 VGPRs, 4 waves/SIMD (k_bb -17 %, A/B)
-#endif
-
-// Phase profile (builds with -DBSGP_PHASE_PROF only): thread 0 of every
-// workgroup adds the shader cycles it spent in each phase to g_phase[slot]
-// (tools/phase_prof.py reads them through bsgp_phase_prof).
-#ifdef BSGP_PHASE_PROF
-__device__ unsigned long long g_phase[kPhaseSlots];
-#define PH_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define PH_ADD(slot, t0)                                                                 \
-  do {                                                                                   \
-    if (threadIdx.x == 0) atomicAdd(&g_phase[slot], __builtin_amdgcn_s_memtime() - (t0)); \
-  } while (0)
-#else
-#define PH_T(v)
-#define PH_ADD(slot, t0)
-#endif
 hipError_t phase_prof(unsigned long long* out, int n, int reset) {
 #ifdef BSGP_PHASE_PROF
   if (n > kPhaseSlots) n = kPhaseSlots;
@@ -99,1260 +30,6 @@ hipError_t phase_prof(unsigned long long* out, int n, int reset) {
   (void)reset;
   return hipErrorNotSupported;
 #endif
-}
-
-// ------------------------------------------------------------------ helpers
-__device__ __forceinline__ double clipX(double x, double lo, double hi) {
-  // X[X < lo] = lo; X[X > hi] = hi  (sgp.py:355-357)
-  double X = (x < lo) ? lo : x;
-  return (X > hi) ? hi : X;
-}
-
-__device__ __forceinline__ double realtime_s() {
-  return (double)__builtin_amdgcn_s_memrealtime() * 1e-8;  // 100 MHz constant clock
-}
-
-// Streaming pass over pixel pairs [0, npair): every thread issues the loads of
-// U pairs before computing any of them (memory-level parallelism for one
-// workgroup streaming a whole image).  `ld(p)` loads, `cp(p, v)` computes.
-template <int U, class LD, class CP>
-__device__ __forceinline__ void stream_range(int p0, int p1, LD&& ld, CP&& cp) {
-  using T = decltype(ld(0));
-  for (int b = p0 + threadIdx.x; b < p1; b += kBlock * U) {
-    T v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int p = b + u * kBlock;
-      if (p < p1) v[u] = ld(p);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int p = b + u * kBlock;
-      if (p < p1) cp(p, v[u]);
-    }
-  }
-}
-// T == 1: the whole image; T > 1: this member's row chunks (Part::cp pairs
-// each), so a pass reads only pixels this member itself produced.
-template <int U, class LD, class CP>
-__device__ __forceinline__ void stream2(const Part& D, int npair, LD&& ld, CP&& cp) {
-  if (D.T == 1) {
-    stream_range<U>(0, npair, ld, cp);
-    return;
-  }
-  for (int p0 = D.m * D.cp; p0 < npair; p0 += D.T * D.cp)
-    stream_range<U>(p0, p0 + D.cp < npair ? p0 + D.cp : npair, ld, cp);
-}
-
-__device__ __forceinline__ double2 ld2(const double* a, int p) {
-  return reinterpret_cast<const double2*>(a)[p];
-}
-
-// Per-image slot vectors (x and g double-buffered; `par` picks the current
-// iterate).  Slot = image: state persists across the phase kernels.
-struct Bufs {
-  double *gns, *bks, *xa, *xb, *ga, *gb, *xtf, *dtf;
-  double* pw;  // den^(beta-1) at the current x_tf (beta objective): reused by the
-               // gradient (k_bb) and the next line search's series moments
-  cd* spec;
-};
-
-__device__ __forceinline__ Bufs slot_bufs(const SolveArgs& A, int img, int par) {
-  Bufs b;
-  double* ws = A.ws + (size_t)img * A.slot_stride;
-  const size_t v = A.vec_stride;
-  b.gns = ws;
-  b.bks = ws + v;
-  double* x0 = ws + 2 * v;
-  double* x1 = ws + 3 * v;
-  double* g0 = ws + 4 * v;
-  double* g1 = ws + 5 * v;
-  b.xa = par ? x1 : x0;
-  b.xb = par ? x0 : x1;
-  b.ga = par ? g1 : g0;
-  b.gb = par ? g0 : g1;
-  b.xtf = ws + 6 * v;
-  b.dtf = ws + 7 * v;
-  b.pw = ws + 8 * v;
-  b.spec = reinterpret_cast<cd*>(ws + 9 * v);
-  return b;
-}
-
-// The search direction of sgp.py:311-318 for one pixel: y = x - alpha*X*g,
-// projected (pflag 1: x(lambda_p) of projectDF(flux, y*D, D); pflag 0: y>=0).
-struct Dir {
-  bool Xones, proj;
-  double alpha, lo, hi, lam_p;
-  ProjClip clip;
-  __device__ __forceinline__ void cd_of(double x, double g, double& c, double& dia) const {
-    const double X = Xones ? 1.0 : clipX(x, lo, hi);
-    const double D = 1 / X;
-    const double y = x - alpha * (X * g);
-    c = y * D;
-    dia = D;
-  }
-  // y = x - alpha*X*g and X of one pixel (sgp.py:311-313)
-  __device__ __forceinline__ void yx(double x, double g, double& y, double& X) const {
-    X = Xones ? 1.0 : clipX(x, lo, hi);
-    y = x - alpha * (X * g);
-  }
-  // x_i(lambda) of projectDF(flux, y*D, D) in multiplier form: (c + lam)/dia
-  // = y + lam*X up to rounding, clipped to [0, sat] (flux_conserve_proj.py:22-25).
-  // The sums of the multiplier search use this form; the projected pixels
-  // themselves (d below) use the reference's division.
-  __device__ __forceinline__ double pv(double y, double X, double lam) const {
-    double v = fma(lam, X, y);
-    v = (0.0 > v) ? 0.0 : v;
-    if (clip.has_sat) v = (clip.satv < v) ? clip.satv : v;
-    return v;
-  }
-  __device__ __forceinline__ double d(double x, double g) const {
-    double y;
-    if (proj) {
-      double c, dia;
-      cd_of(x, g, c, dia);
-      y = clip(c, dia, lam_p);
-    } else {
-      const double X = Xones ? 1.0 : clipX(x, lo, hi);
-      y = x - alpha * (X * g);
-      if (y < 0) y = 0;
-    }
-    return y - x;
-  }
-};
-
-__device__ __forceinline__ Dir make_dir(const SolveArgs& A, const ImgState& st) {
-  Dir D;
-  D.Xones = st.Xones != 0;
-  D.proj = A.prm.proj_type == 1;
-  D.alpha = st.alpha;
-  D.lo = st.lo;
-  D.hi = st.hi;
-  D.lam_p = st.lam_p;
-  D.clip = ProjClip{A.prm.has_sat != 0, A.prm.ccd_sat_level / st.sc - 2.220446049250313e-16};
-  // float32 image, proj_type 0: the first scaling matrix is x.copy() of the
-  // float32 start, clipped (compared and assigned) at float32 bounds
-  // (sgp.py:279-285 / 723-729); from iteration 2 on x is float64
-  if (A.prm.gn_f32 && A.prm.proj_type == 0 && st.iter == 1) {
-    D.lo = (double)(float)st.lo;
-    D.hi = (double)(float)st.hi;
-  }
-  return D;
-}
-
-__device__ __forceinline__ Objective make_obj(const SolveArgs& A, double beta) {
-  Objective o;
-  o.variant = A.prm.variant;
-  o.f32g = A.prm.gn_f32 != 0;
-  o.set_beta(beta);
-  return o;
-}
-
-// Team of the workgroup: members blockIdx.x % T of image img0 + blockIdx.x / T.
-__device__ __forceinline__ Team make_team(const SolveArgs& A, int img, const ImgState& st) {
-  Team t;
-  t.T = A.T;
-  t.m = A.T == 1 ? 0 : (int)(blockIdx.x % (unsigned)A.T);
-  t.part = A.tpart ? A.tpart + (size_t)img * 2 * A.T * kMaxRed : nullptr;
-  t.ctr = A.tctr ? A.tctr + img : nullptr;
-  t.base = (unsigned int)st.bar_base;
-  t.nb = 0;
-  t.fail = A.tfail;
-  return t;
-}
-__device__ __forceinline__ int team_img(const SolveArgs& A) {
-  return A.img0 + (A.T == 1 ? (int)blockIdx.x : (int)(blockIdx.x / (unsigned)A.T));
-}
-// Member 0 records where the barrier counter stands for the next kernel; all
-// members read bar_base before their first arrival, member 0 writes it after
-// its last one, so no member can see the new value early.
-__device__ __forceinline__ void team_end(ImgState& st, const Team& t) {
-  if (t.T > 1 && t.m == 0 && threadIdx.x == 0 && t.nb > 0)
-    st.bar_base = (int)(t.base + (unsigned int)t.T * (unsigned int)t.nb);
-}
-__device__ __forceinline__ bool leader(const Team& t) { return t.m == 0 && threadIdx.x == 0; }
-
-#define BSGP_LDS_VIEWS(A)                                                           \
-  extern __shared__ __attribute__((aligned(16))) char smem[];                      \
-  cd* lds = reinterpret_cast<cd*>(smem);                                           \
-  double* red = reinterpret_cast<double*>(smem + (A).lds_fft_bytes)
-
-// numpy's float32 np.sum of term(i) for i < N, in numpy's exact order (the
-// plan's PwProg, bsgp_api.hip pairwise_program): the leaves by the team's
-// threads (each a numpy leaf: 8 strided float32 accumulators), the inner nodes
-// level by level with a team barrier between levels, then the chunk fold
-// res = res + root from 0.  `vals` is float scratch in HBM (leaves + nodes).
-template <class TERM>
-__device__ float np_f32_sum(const PwProg& pw, TERM&& term, float* vals, const Part& D, Team& tm) {
-  const int* lv = pw.prog;
-  const int* nd = lv + 2 * pw.nleaf;
-  const int* off = nd + 2 * pw.nnode;
-  const int* roots = off + pw.nlev + 1;
-  for (int l = D.gt0 + (int)threadIdx.x; l < pw.nleaf; l += D.gts) {
-    const int s0 = lv[2 * l], n = lv[2 * l + 1];
-    float res;
-    if (n < 8) {
-      res = 0.0f;
-      for (int i = 0; i < n; ++i) res += term(s0 + i);
-    } else {
-      float r[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = term(s0 + j);
-      int i = 8;
-      for (; i < n - (n % 8); i += 8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] += term(s0 + i + j);
-      }
-      res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-      for (; i < n; ++i) res += term(s0 + i);
-    }
-    vals[l] = res;
-  }
-  team_sync(tm);
-  for (int h = 0; h < pw.nlev; ++h) {
-    for (int k = off[h] + D.gt0 + (int)threadIdx.x; k < off[h + 1]; k += D.gts)
-      vals[pw.nleaf + k] = vals[nd[2 * k]] + vals[nd[2 * k + 1]];
-    team_sync(tm);
-  }
-  float res = 0.0f;
-  for (int c = 0; c < pw.nchunk; ++c) res = res + vals[roots[c]];
-  return res;
-}
-
-// ------------------------------------------------------------ kernel: setup
-// sgp.py:163-298 (= 617-742): scaling, null pixels, flux, x0, initial
-// projection, x_tf = A(x), f, g and the scaling-matrix bounds.
-template <bool COOP>
-__global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
-  BSGP_LDS_VIEWS(A);
-  const int img = team_img(A);
-  const Geo& G = A.g;
-  const bsgp_params& P = A.prm;
-  const int N = G.H * G.W;
-  const int tid = threadIdx.x;
-  const bool bmap = P.bkg_is_map != 0;
-  const bool odd = (N & 1) != 0;
-  Bufs B = slot_bufs(A, img, 0);
-  ImgState& st = A.st[img];
-  // counters are zeroed per solve: the setup kernel starts the count at 0
-  Team tm = make_team(A, img, st);
-  tm.base = 0;
-  const Part D = make_part(tm, G.nfw, G.W);
-  load_tw_lds(G);
-  const double* gn_in = A.in.gn + (size_t)img * N;
-  const double* bk_in = bmap ? A.in.bkg + (size_t)img * N : nullptr;
-  const double bk_scalar_raw = bmap ? 0.0 : A.in.bkg[img];
-  const double t0 = realtime_s();
-
-  // raw statistics (sgp.py:174-177, 190, 193-194)
-  double v2[2] = {0.0, 0.0};  // sum(gn - bkg), sum(gn)
-  double mx = -INFINITY;
-  double ok32 = 1.0;  // every raw value finite and exact in f32 (params.gn_compact)
-  for (int i = D.gt0 + tid; i < N; i += D.gts) {
-    const double g = gn_in[i];
-    const double bkr = bmap ? bk_in[i] : bk_scalar_raw;
-    v2[0] += g - bkr;
-    v2[1] += g;
-    mx = (g > mx || g != g) ? g : mx;
-    if (!(isfinite(g) && (double)(float)g == g)) ok32 = 0.0;
-  }
-  team_sum<2>(v2, red, tm);
-  mx = team_max(mx, red, tm);
-  if (P.gn_compact) ok32 = team_min(ok32, red, tm);
-  const double sc = P.scale_data == 2 ? P.prescaled_scaling : (P.scale_data ? mx : 1.0);
-  const double fl_raw = A.in.flux ? A.in.flux[img] : v2[0];
-  const double x3 = (fl_raw / (double)N) * 1.0;  // np.sum(gn-bkg)/gn.size*ones (sgp.py:175)
-  const double tol4 = P.scale_data == 2 ? P.prescaled_tol4 : 1 + 1 / (v2[1] / (double)N);
-  const bool divide = P.scale_data == 1;
-  const double bks_scalar = P.scale_data == 2 ? bk_scalar_raw : bk_scalar_raw / sc;
-  // scale + null-pixel minimum (sgp.py:193-204)
-  double vmin = INFINITY;
-  for (int i = D.gt0 + tid; i < N; i += D.gts) {
-    const double g = divide ? gn_in[i] / sc : gn_in[i];
-    B.gns[i] = g;
-    if (g > 0 && g < vmin) vmin = g;
-    if (bmap) B.bks[i] = divide ? bk_in[i] / sc : bk_in[i];
-  }
-  vmin = team_min(vmin, red, tm);
-  const double eps = 2.220446049250313e-16;
-  const double fill = vmin * eps * eps;
-  double v1[1] = {0.0};
-  for (int i = D.gt0 + tid; i < N; i += D.gts) {
-    double g = B.gns[i];
-    if (g <= 0) {
-      g = fill;
-      B.gns[i] = g;
-    }
-    v1[0] += g - (bmap ? B.bks[i] : bks_scalar);
-    // initial x (sgp.py:166-177, 197), then the pflag==0 clamp (:248-249)
-    double x;
-    if (A.in.x0) {
-      x = A.in.x0[(size_t)img * N + i];
-    } else if (P.init_recon == 0) {
-      x = 0.0;
-    } else if (P.init_recon == 2) {
-      x = gn_in[i];
-    } else {
-      x = x3;
-    }
-    if (divide) x = x / sc;
-    if (P.proj_type == 0 && x < 0) x = 0;
-    B.xa[i] = x;
-  }
-  if (odd && leader(tm)) {  // benign pad element of the pair-vectorised streams
-    B.gns[N] = 1.0;
-    if (bmap) B.bks[N] = 0.0;
-    B.xa[N] = B.xb[N] = B.ga[N] = B.gb[N] = B.xtf[N] = B.dtf[N] = 0.0;
-  }
-  team_sum<1>(v1, red, tm);
-  // sgp.py:208-211 (scale_data 2: the caller scaled the flux in its own dtype)
-  const double flux =
-      A.in.flux ? (P.scale_data == 2 ? A.in.flux[img] : A.in.flux[img] / sc) : v1[0];
-  const ProjClip clip{P.has_sat != 0, P.ccd_sat_level / sc - eps};
-
-  // initial projection with dia = 1 (sgp.py:250-253); every thread clips the
-  // pixels it wrote, so only the rows pass below needs the team barrier
-  if (P.proj_type == 1) {
-    auto psum = [&](double lam) {
-      double s1[1] = {0.0};
-      for (int i = D.gt0 + tid; i < N; i += D.gts) s1[0] += clip(B.xa[i], 1.0, lam);
-      team_sum<1>(s1, red, tm);
-      return s1[0];
-    };
-    ProjOut po = project_df_fn(psum, flux, 0.0, 1.0, 1e-11, 0, 0, P.max_projs);
-    for (int i = D.gt0 + tid; i < N; i += D.gts) B.xa[i] = clip(B.xa[i], 1.0, po.lam);
-  }
-  team_sync(tm);  // x0 / gns / bks complete before the row passes
-  // x_tf = A(x), f and g (sgp.py:260-265 / 702-709)
-  const double beta0 = A.in.beta0 ? A.in.beta0[img] : P.betaParam;
-  Objective obj = make_obj(A, beta0);
-  // float32 image: the lambda-independent sum np.sum(s*gn**beta) is a float32
-  // array reduced by numpy in float32 (sgp.py:458); its order is the plan's
-  // pairwise program.  The dtf vector is free scratch until the first k_ls.
-  const bool konst_f32 = P.gn_f32 && P.variant == BSGP_VARIANT_BETA && obj.mode == 3;
-  double konst32 = 0.0;
-  if (konst_f32) {
-    const float sf = (float)obj.scal;
-    const double bf = (double)(float)obj.beta;  // x**beta: the exponent is cast to float32
-    konst32 = (double)np_f32_sum(
-        A.pw, [&](int i) { return sf * (float)pow(B.gns[i], bf); },
-        reinterpret_cast<float*>(B.dtf), D, tm);
-  }
-  double fsum[3] = {0.0, 0.0, 0.0};  // K, T0, T1
-  row_fwd<COOP>(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.xa[r * G.W + j]; });
-  team_sync(tm);
-  col_conv<COOP>(G, D, B.spec, tf_of(G, img, 0), lds);
-  team_sync(tm);
-  const bool beta_obj = P.variant == BSGP_VARIANT_BETA;
-  row_inv_fwd<COOP>(G, D, B.spec, lds, [&](int r, int j, double v) {
-    const int i = r * G.W + j;
-    B.xtf[i] = v;
-    const double den = v + (bmap ? B.bks[i] : bks_scalar);
-    const double g = B.gns[i];
-    fsum[0] += obj.konst(g);
-    obj.terms(v, den, g, &fsum[1]);
-    if (!beta_obj) return g / den;  // KL: w = gn/den (sgp.py:262)
-    const double p = fpow(den, obj.beta - 1);
-    B.pw[i] = p;
-    return g * (p / den);  // gn*den^(b-2) (sgp.py:499)
-  });
-  team_sum<3>(fsum, red, tm);
-  team_sync(tm);  // publishes xtf / spec / pw
-  if (konst_f32) fsum[0] = konst32;
-  const double fv = obj.combine(fsum[0], fsum[1], fsum[2], flux, (double)N);
-  col_conv<COOP>(G, D, B.spec, tf_of(G, img, 1), lds);
-  team_sync(tm);
-  row_inv<COOP>(G, D, B.spec, lds, [&](int r, int j, double at) {
-    const int i = r * G.W + j;
-    B.ga[i] = (beta_obj ? B.pw[i] : 1.0) - at;  // sgp.py:263 / 499
-  });
-  team_sync(tm);  // every row of spec read before it is overwritten
-  // scaling-matrix bounds from AT(gn) (sgp.py:268-273)
-  row_fwd<COOP>(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.gns[r * G.W + j]; });
-  team_sync(tm);
-  col_conv<COOP>(G, D, B.spec, tf_of(G, img, 1), lds);
-  team_sync(tm);
-  double ymin = INFINITY, ymax = -INFINITY;
-  row_inv<COOP>(G, D, B.spec, lds, [&](int r, int j, double at) {
-    const int i = r * G.W + j;
-    const double bkv = bmap ? B.bks[i] : bks_scalar;
-    const double y = (flux / (flux + bkv)) * at;
-    if (y > 0 && y < ymin) ymin = y;
-    ymax = (y > ymax || y != y) ? y : ymax;
-  });
-  ymin = team_min(ymin, red, tm);
-  ymax = team_max(ymax, red, tm);
-  double lo = ymin, hi = ymax;
-  if (hi / lo < 50) {
-    lo = lo / 10;
-    hi = hi * 10;
-  }
-  // Compact observed image: the raw f32-exact values replace gn_s in the first
-  // half of its slot vector (every f64 read of gn_s is done: team_sync above).
-  // Readers recompute gn_s = raw / sc (or raw), and the null-pixel fill for
-  // raw <= 0, with the operations used above: the same bits as f64 storage.
-  const int g32 = (P.gn_compact && ok32 > 0.5) ? (divide ? (sc > 0 ? 2 : 0) : 1) : 0;
-  if (g32) {
-    float* gf = reinterpret_cast<float*>(B.gns);
-    for (int i = D.gt0 + tid; i < N; i += D.gts) gf[i] = (float)gn_in[i];
-    if (odd && leader(tm)) gf[N] = 1.0f;  // pad element of the pair-vectorised streams
-  }
-  const double Dcoeff = 2 / (double)N * sc;
-  double tol = P.tol_convergence;
-  if (P.stop_criterion == 4) tol = tol4;
-  if (P.verbose && P.stop_criterion == 2) tol = tol * tol;
-  if (leader(tm)) {
-    const int M1 = P.MAXIT + 1;
-    A.out.discr[(size_t)img * M1] = Dcoeff * fv;
-    if (A.out.times) A.out.times[(size_t)img * M1] = 0.0;
-    if (A.out.crit) A.out.crit[(size_t)img * M1] = 0.0;
-    if (A.out.flags) A.out.flags[(size_t)img * M1] = 0;
-    for (int k = 0; k < P.M_alpha; ++k) st.Valpha[k] = P.alpha_max;
-    for (int k = 0; k < P.M; ++k) st.Fold[k] = -1e30;
-    st.par = 0;
-    st.Xones = P.init_recon == 0;  // X = ones until the first BB update (sgp.py:279-280)
-    st.stop = 0;
-    st.iter = 1;
-    st.epoch = 0;
-    st.bar_base = (int)((unsigned int)tm.T * (unsigned int)tm.nb);
-    st.E_p = st.E_ls = st.ls_passes = st.status = st.ls_series = 0;
-    st.proj_passes = st.proj_list = 0;
-    st.lam_p = 0.0;  // no previous multiplier: the first projection splits no bracket
-    st.sc = sc;
-    st.flux = flux;
-    st.bks_scalar = bks_scalar;
-    st.lo = lo;
-    st.hi = hi;
-    st.Dcoeff = Dcoeff;
-    st.tol = tol;
-    st.t0 = t0;
-    st.fv = fv;
-    st.alpha = P.alpha;
-    st.tau = P.tau;
-    st.lr = P.lr;
-    st.init_lr = P.lr;
-    st.beta = beta0;
-    st.konst = fsum[0];
-    st.g32 = g32;
-    st.gfill = fill;
-    atomicAdd(A.active, 1);
-  }
-}
-
-// --------------------------------------- projection with pixel lists
-// projectDF(flux, y*D, D) (flux_conserve_proj.py:7-144) for the direction of
-// sgp.py:311-318: the reference's multiplier sequence, step for step
-// (project_df_fn).  What changes is how sum_i x_i(lambda) is evaluated:
-//  * the first evaluation (lambda_ = 0) is a full pass over (x, g) that also
-//    sums x(lambda_ - dlambda_) and x(lambda_ + dlambda_), the second
-//    evaluation of either bracketing branch (:32 / :57), and the slope at
-//    lambda_ (for a Newton bound on the root);
-//  * a full pass can split the pixels for a bracket [qL, qU]: pixels at 0 or
-//    at saturation for every lambda in it add a constant, pixels strictly
-//    inside add y + lambda*X (two running sums), and only the pixels that
-//    change state inside the bracket go to this thread's list (y, X);
-//  * an evaluation whose lambda lies in the split bracket reads only the list
-//    (typically 2-5% of the pixels, written and read back by the same thread).
-// Split brackets: the previous iteration's multiplier +/- 30% on the first
-// pass; on the first miss, the hull of the missing lambda and the Newton
-// bound (for the convex sum the secant and Newton iterates fall on either
-// side of the root); on later misses, the tightest bracket of signs seen.
-// A miss is just a full pass, so the choice of bracket never changes results.
-#ifndef BSGP_PROJ_GUESS_W
-#define BSGP_PROJ_GUESS_W 0.3
-#endif
-constexpr double kProjGuessW = BSGP_PROJ_GUESS_W;
-
-__device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt, Team& tm,
-                                     const Dir& D, const Bufs& B, double* red, double lam_prev,
-                                     double flux, int npair, bool odd, int N, int64_t& passes,
-                                     int64_t& list_reads) {
-  const double* xa = B.xa;
-  const double* ga = B.ga;
-  const int LS = tm.T * kBlock;
-  const int gt = tm.m * kBlock + (int)threadIdx.x;
-  double* ly = A.plist + (size_t)img * A.plist_stride;
-  double* lX = ly + A.plist_stride / 2;
-  const int lcap = A.lcap;
-  const bool hs = D.clip.has_sat;
-  const double satv = D.clip.satv;
-  // identical in every thread of the team
-  bool have = false;
-  double cL = 0.0, cU = 0.0, SA = 0.0, SB = 0.0, nsat = 0.0, nstr = 0.0;
-  double Lk = -INFINITY, Uk = INFINITY;  // largest lambda with r < 0, smallest with r > 0
-  double xl0 = NAN, xs0 = 0.0, xl1 = NAN, xs1 = 0.0, lamN = NAN;
-  bool first_miss = true;
-  int calls = 0;
-  int cnt = 0;  // this thread's list entries
-
-  auto note = [&](double lam, double S) {
-    const double r = S - flux;
-    if (r < 0 && lam > Lk) Lk = lam;
-    if (r > 0 && lam < Uk) Uk = lam;
-  };
-  // One full pass: sums at lams[0..NL), optional split for [qL, qU]; returns
-  // the slope sum_{0 < x_i(lams[0]) < sat} X_i.
-  auto pass = [&](auto nlc, const double* lams, double* S, bool split, double qL,
-                  double qU) -> double {
-    constexpr int NL = decltype(nlc)::value;
-    constexpr int NT = NL + 6;  // sums | SA, SB, n_sat, n_list, n_overflow | slope
-    PH_T(tp0);
-    double t[NT];
-#pragma unroll
-    for (int k = 0; k < NT; ++k) t[k] = 0.0;
-    double lm[NL];
-#pragma unroll
-    for (int k = 0; k < NL; ++k) lm[k] = lams[k];
-    if (split) cnt = 0;
-    auto px = [&](double x, double g) __attribute__((always_inline)) {
-      double y, X;
-      D.yx(x, g, y, X);
-#pragma unroll
-      for (int k = 0; k < NL; ++k) {
-        const double v = D.pv(y, X, lm[k]);
-        t[k] += v;
-        if (k == 0 && v > 0.0 && (!hs || v < satv)) t[NL + 5] += X;
-      }
-      if (split) {
-        const double vL = D.pv(y, X, qL), vU = D.pv(y, X, qU);
-        if (vU == 0.0) {
-          // 0 for every lambda <= qU
-        } else if (hs && vL == satv) {
-          t[NL + 2] += 1.0;  // saturated for every lambda >= qL
-        } else if (vL > 0.0 && (!hs || vU < satv)) {
-          t[NL] += y;  // unclipped over the whole bracket
-          t[NL + 1] += X;
-        } else if (cnt < lcap) {
-          ly[(size_t)cnt * LS + gt] = y;
-          lX[(size_t)cnt * LS + gt] = X;
-          ++cnt;
-          t[NL + 3] += 1.0;
-        } else {
-          t[NL + 4] += 1.0;
-        }
-      }
-    };
-    stream2<BSGP_PROJ_U>(
-        Pt, npair,
-        [&](int p) {
-          struct V {
-            double2 x, g;
-          } v;
-          v.x = ld2(xa, p);
-          v.g = ld2(ga, p);
-          return v;
-        },
-        [&](int p, const auto& v) {
-          px(v.x.x, v.g.x);
-          if (!odd || 2 * p + 1 < N) px(v.x.y, v.g.y);
-        });
-    // the list is read back by the thread that wrote it: drain its stores
-    if (split) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    team_sum<NT>(t, red, tm);
-#pragma unroll
-    for (int k = 0; k < NL; ++k) S[k] = t[k];
-    if (split) {
-      have = t[NL + 4] == 0.0;
-      cL = qL;
-      cU = qU;
-      SA = t[NL];
-      SB = t[NL + 1];
-      nsat = t[NL + 2];
-      nstr = t[NL + 3];
-    }
-    ++passes;
-    PH_ADD(NL == 3 ? 10 : 12, tp0);
-    return t[NL + 5];
-  };
-  // sum over the split bracket's list
-  auto leval = [&](double lam) {
-    PH_T(tl0);
-    double t[1] = {0.0};
-    int k = 0;
-    for (; k + 4 <= cnt; k += 4) {
-      double yv[4], Xv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        yv[u] = ly[(size_t)(k + u) * LS + gt];
-        Xv[u] = lX[(size_t)(k + u) * LS + gt];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) t[0] += D.pv(yv[u], Xv[u], lam);
-    }
-    for (; k < cnt; ++k) t[0] += D.pv(ly[(size_t)k * LS + gt], lX[(size_t)k * LS + gt], lam);
-    team_sum<1>(t, red, tm);
-    PH_ADD(11, tl0);
-    const double lin = SA + lam * SB;
-    return (hs ? lin + nsat * satv : lin) + t[0];
-  };
-  auto sumf = [&](double lam) {
-    double S;
-    if (calls == 0) {
-      const double lams[3] = {lam, lam - 1.0, lam + 1.0};  // lambda_ -/+ dlambda_ (dlambda_ = 1)
-      double Sv[3];
-      const bool guess = isfinite(lam_prev) && lam_prev != 0.0;
-      const double w = kProjGuessW * fabs(lam_prev);
-      const double slope = pass(std::integral_constant<int, 3>{}, lams, Sv, guess,
-                                lam_prev - w, lam_prev + w);
-      S = Sv[0];
-      xl0 = lams[1];
-      xs0 = Sv[1];
-      xl1 = lams[2];
-      xs1 = Sv[2];
-      note(lams[1], Sv[1]);
-      note(lams[2], Sv[2]);
-      lamN = slope > 0.0 ? lam - (S - flux) / slope : NAN;
-    } else if (lam == xl0) {
-      S = xs0;
-    } else if (lam == xl1) {
-      S = xs1;
-    } else if (have && lam >= cL && lam <= cU) {
-      S = leval(lam);
-      list_reads += (int64_t)nstr;
-    } else {
-      bool split = false;
-      double qL = 0.0, qU = 0.0;
-      if (first_miss && isfinite(lamN)) {
-        qL = fmin(lam, lamN);
-        qU = fmax(lam, lamN);
-        split = true;
-      } else if (isfinite(Lk) && isfinite(Uk)) {
-        qL = fmin(Lk, Uk);
-        qU = fmax(Lk, Uk);
-        split = true;
-      }
-      first_miss = false;
-      const double lams[1] = {lam};
-      double Sv[1];
-      (void)pass(std::integral_constant<int, 1>{}, lams, Sv, split, qL, qU);
-      S = Sv[0];
-    }
-    ++calls;
-    note(lam, S);
-    return S;
-  };
-  return project_df_fn(sumf, flux, 0.0, 1.0, 1e-11, 0, 0, A.prm.max_projs);
-}
-
-// ------------------------------------------ kernel: direction + rows of d
-// sgp.py:306-325: memory shifts, y = x - alpha*X*g, projectDF(flux, y*D, D)
-// with every x(lambda) evaluation one streaming pass over (x, g), d = y - x,
-// d.g, and the row transforms of d.
-template <bool COOP>
-__global__ void __launch_bounds__(kBlock) BSGP_DIR_ATTR k_dir(SolveArgs A) {
-  BSGP_LDS_VIEWS(A);
-  const int img = team_img(A);
-  ImgState& st = A.st[img];
-  if (st.stop) return;
-  PH_T(tk0);
-  Team tm = make_team(A, img, st);
-  const Geo& G = A.g;
-  const Part Pt = make_part(tm, G.nfw, G.W);
-  load_tw_lds(G);
-  const bsgp_params& P = A.prm;
-  const int N = G.H * G.W;
-  const int npair = (N + 1) / 2;
-  const bool odd = (N & 1) != 0;
-  Bufs B = slot_bufs(A, img, st.par);
-  Dir D = make_dir(A, st);
-  const double flux = st.flux;
-  int evals = 0;
-  int64_t ppass = 0, plist_reads = 0;
-  if (P.proj_type == 1 && A.plist != nullptr) {
-    ProjOut po = cached_projection(A, img, Pt, tm, D, B, red, st.lam_p, flux, npair, odd, N,
-                                   ppass, plist_reads);
-    D.lam_p = po.lam;
-    evals = po.evals;
-  } else if (P.proj_type == 1) {
-    const double* xa = B.xa;
-    const double* ga = B.ga;
-    auto psum = [&](double lam) {
-      double s[1] = {0.0};
-      stream2<4>(
-          Pt, npair,
-          [&](int p) {
-            struct V {
-              double2 x, g;
-            } v;
-            v.x = ld2(xa, p);
-            v.g = ld2(ga, p);
-            return v;
-          },
-          [&](int p, const auto& v) {
-            double c, d;
-            D.cd_of(v.x.x, v.g.x, c, d);
-            s[0] += D.clip(c, d, lam);
-            if (!odd || 2 * p + 1 < N) {
-              D.cd_of(v.x.y, v.g.y, c, d);
-              s[0] += D.clip(c, d, lam);
-            }
-          });
-      team_sum<1>(s, red, tm);
-      return s[0];
-    };
-    ProjOut po = project_df_fn(psum, flux, 0.0, 1.0, 1e-11, 0, 0, P.max_projs);
-    D.lam_p = po.lam;
-    evals = po.evals;
-    ppass = po.evals;
-  }
-  PH_ADD(0, tk0);
-  PH_T(tk1);
-  double gd[1] = {0.0};
-  row_fwd2<BSGP_DIR_JCH, BSGP_DIR_PF, BSGP_DIR_COMP, COOP>(
-      G, Pt, G.H, G.W, G.H, B.spec, lds,
-      [&](int r, int j) {
-        const int i = r * G.W + j;
-        return double2{B.xa[i], B.ga[i]};
-      },
-      [&](int, int, const double2& v) {
-        const double d = D.d(v.x, v.y);
-        gd[0] += d * v.y;
-        return d;
-      });
-  team_sum<1>(gd, red, tm);
-  PH_ADD(1, tk1);
-  if ((BSGP_FUSE_COL & 1) && (A.fuse_col & 1)) {  // T == 1: A's column pass follows here
-    PH_T(tc0);
-    team_sync(tm);
-    col_conv<COOP>(G, Pt, B.spec, tf_of(G, img, 0), lds);
-    PH_ADD(3, tc0);
-  }
-  PH_ADD(2, tk0);
-  team_end(st, tm);
-  if (leader(tm)) {  // sgp.py:306-308 (memory shifts) + direction scalars
-    for (int k = 0; k < P.M_alpha - 1; ++k) st.Valpha[k] = st.Valpha[k + 1];
-    for (int k = 0; k < P.M - 1; ++k) st.Fold[k] = st.Fold[k + 1];
-    st.Fold[P.M - 1] = st.fv;
-    st.epoch += 1;
-    st.lam_p = D.lam_p;
-    st.E_p += evals;
-    st.proj_passes += ppass;
-    st.proj_list += plist_reads;
-    st.gd = gd[0];
-  }
-}
-
-// ----------------------------------------------------------- kernel: columns
-template <bool COOP>
-__global__ void __launch_bounds__(kBlock) BSGP_COL_ATTR k_col(SolveArgs A, int transpose) {
-  BSGP_LDS_VIEWS(A);
-  // A.Tc workgroups per image (>= the team size T): columns only, no barrier
-  const int img = A.img0 + (A.Tc == 1 ? (int)blockIdx.x : (int)(blockIdx.x / (unsigned)A.Tc));
-  const ImgState& st = A.st[img];
-  if (st.stop) return;
-  PH_T(tc0);
-  Team tm{};
-  tm.T = A.Tc;
-  tm.m = A.Tc == 1 ? 0 : (int)(blockIdx.x % (unsigned)A.Tc);
-  Bufs B = slot_bufs(A, img, 0);
-  load_tw_lds(A.g);
-  col_conv<COOP>(A.g, make_part(tm, A.g.nfw, A.g.W), B.spec, tf_of(A.g, img, transpose), lds);
-  PH_ADD(3, tc0);
-}
-
-// ------------------------------- kernel: line search + accept + rows of w
-// sgp.py:326-349 / 774-801: K trial lambdas per pass over (x_tf, d_tf, gn);
-// the first pass is fused into the inverse row transforms that produce d_tf.
-// Then x_tf += lam*d_tf and the row transforms of AT's input w.
-template <int K, int MODE, bool ADAPT, bool COOP>
-__global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
-  // first pass (fused into the inverse rows of A(d)): one trial lambda = 1,
-  // which is where most non-stagnating iterations accept; later passes
-  // stream K trial lambdas each.
-  BSGP_LDS_VIEWS(A);
-  const int img = team_img(A);
-  ImgState& st = A.st[img];
-  if (st.stop) return;
-  PH_T(tk0);
-  Team tm = make_team(A, img, st);
-  const Geo& G = A.g;
-  const Part Pt = make_part(tm, G.nfw, G.W);
-  load_tw_lds(G);
-  const bsgp_params& P = A.prm;
-  const int N = G.H * G.W;
-  const int npair = (N + 1) / 2;
-  const bool odd = (N & 1) != 0;
-  const bool bmap = P.bkg_is_map != 0;
-  const double lr_st = st.lr;
-  constexpr bool adapt = ADAPT;  // adaptive beta (sgp.py:798-800): K == 1, runtime mode
-  Bufs B = slot_bufs(A, img, st.par);
-  if ((BSGP_FUSE_COL & 4) && (A.fuse_col & 4)) {  // T == 1: A's column pass of k_dir's rows
-    PH_T(tc0);
-    col_conv<COOP>(G, Pt, B.spec, tf_of(G, img, 0), lds);
-    team_sync(tm);
-    PH_ADD(3, tc0);
-  }
-  const double bks_scalar = st.bks_scalar;
-  const double flux = st.flux;
-  const double gd = st.gd;
-  // compact gn (ImgState::g32): loaders fetch the raw f32, users decode it
-  const int g32 = st.g32;
-  const double gsc = st.sc, grc = 1.0 / st.sc, gfill = st.gfill;
-  const float* gnf = reinterpret_cast<const float*>(B.gns);
-  // (the raw f32 travels in the low word of the f64 operand register, so both
-  // storage modes use the same registers)
-  auto gdec1 = [&](float v) __attribute__((always_inline)) {
-    const double g = v;
-    return g > 0 ? (g32 == 2 ? div_rn(g, gsc, grc) : g) : gfill;
-  };
-  auto gdec = [&](double r) __attribute__((always_inline)) {
-    return g32 ? gdec1(__int_as_float(__double2loint(r))) : r;
-  };
-  auto gload = [&](int i) __attribute__((always_inline)) {
-    return g32 ? __hiloint2double(0, __float_as_int(gnf[i])) : B.gns[i];
-  };
-  double fr = st.Fold[0];
-  for (int k = 1; k < P.M; ++k) fr = py_max2(fr, st.Fold[k]);
-  const int ls_cap = A.ls_cap;  // trial cap (bsgp_api.hip): never reached for 0 < beta < 1
-  Objective obj = make_obj(A, st.beta);
-  double lam = 1.0;
-  double f_acc = 0.0;
-  int nls = 0, passes = 0, status = 0, series_evals = 0;
-  bool accepted = false;
-  constexpr int NT = 2 * K + 2;  // [2k],[2k+1]: lambda_k sums; [2K]: const; [2K+1]: dDiv/dbeta
-  // The lambda-independent sum (sum s*gn^b, or sum gn at beta = 1) is carried
-  // in the state; with adaptive beta it changes with beta and is recomputed.
-  double konst = st.konst;
-  // Small-step series (general beta, fixed beta): with den_i(lam) =
-  // a_i (1 + lam u_i), a_i = x_tf_i + bkg_i, u_i = d_tf_i / a_i,
-  //   sum den^b        = sum_m binom(b, m)   lam^m P_m,  P_m = sum a^b u^m
-  //   sum gn den^(b-1) = sum_m binom(b-1, m) lam^m Q_m,  Q_m = sum gn a^(b-1) u^m
-  // so every trial with lam * max|u| <= kSeriesRho is evaluated without a pass
-  // over the image (truncation < 1e-17 relative at MS = 6: (0.01)^7 * binom).
-  constexpr int MS = 6;
-  constexpr double kSeriesRho = 0.01;
-  const bool series = (MODE == 3 || MODE == 4) && !adapt && P.ls_series != 0;
-  // the moments and binomial coefficients are the same in every thread: they
-  // live in LDS after the first pass (ser[0..3][MS+1] = P, Q, binom(b, m),
-  // binom(b-1, m)), not in VGPRs across the trial passes
-  double* ser = red + kWaves * kMaxRed + kMaxRed + 8;
-  double rho = INFINITY;
-  // ---- pass 1, fused into the inverse rows that produce d_tf: lam = 1 direct
-  {
-    constexpr int N1 = 4 + 2 * (MS + 1);  // lam=1 sums, const, dDiv/dbeta, P_m, Q_m
-    double t1[N1];
-#pragma unroll
-    for (int k = 0; k < N1; ++k) t1[k] = 0.0;
-    double umax = 0.0;
-    struct LsIn {
-      double x0, g, p0, bkv;
-    };
-    row_inv2<BSGP_LS1_PRE, BSGP_LS1_JCH, BSGP_LS_COMP, COOP>(
-        G, Pt, B.spec, lds,
-        [&](int r, int j) {
-          const int i = r * G.W + j;
-          LsIn q;
-          q.x0 = B.xtf[i];
-          q.g = gload(i);
-          q.p0 = series ? B.pw[i] : 0.0;
-          q.bkv = bmap ? B.bks[i] : bks_scalar;
-          return q;
-        },
-        [&](int r, int j, double v, const LsIn& q) {
-      const int i = r * G.W + j;
-      B.dtf[i] = v;
-      const double g = gdec(q.g);
-      const double x0 = q.x0;
-      const double bkv = q.bkv;
-      const double xt = x0 + lam * v;
-      obj.template terms_m<MODE>(xt, xt + bkv, g, &t1[0]);
-      if constexpr (adapt) {
-        t1[2] += obj.konst(g);
-        t1[3] += beta_deriv_px(xt + bkv, g, obj.beta);
-      }
-      if (series) {
-        const double a = x0 + bkv;
-        const double u = v / a;
-        const double p0 = q.p0;  // = fpow(a, beta-1), stored at the last accept
-        // MODE 4: the float32-rounded (s*b)*gn factor; combined without c2 below
-        const double A0 = a * p0, B0 = (MODE == 4 ? (double)(obj.c2f * (float)g) : g) * p0;
-        double um = 1.0;
-#pragma unroll
-        for (int m = 0; m <= MS; ++m) {
-          t1[4 + m] += A0 * um;
-          t1[4 + MS + 1 + m] += B0 * um;
-          um *= u;
-        }
-        const double au = fabs(u);
-        umax = (au > umax || au != au || !(a > 0)) ? (a > 0 ? au : INFINITY) : umax;
-      }
-    });
-    team_sum<N1>(t1, red, tm);
-    if (series) rho = team_max(umax, red, tm);
-    PH_ADD(4, tk0);
-    if (series && threadIdx.x == 0) {
-      for (int m = 0; m <= MS; ++m) {
-        ser[m] = t1[4 + m];
-        ser[MS + 1 + m] = t1[4 + MS + 1 + m];
-      }
-    }
-    if (adapt) konst = t1[2];
-    ++passes;
-    ++nls;
-    const double f1 = obj.combine(konst, t1[0], t1[1], flux, (double)N);
-    if (f1 <= fr + P.gamma * lam * gd || lam < 1e-12) {
-      f_acc = f1;
-      accepted = true;
-    } else {
-      lam = lam * P.beta;
-      if (adapt) {  // sgp.py:798-800: beta -= lr * mean(dDiv/dbeta)
-        const double bgrad = (obj.beta == 0.0 || obj.beta == 1.0) ? 0.0 : t1[3] / N;
-        obj.set_beta(obj.beta - lr_st * bgrad);
-      }
-    }
-  }
-  // binomial coefficients of the series
-  if (series && threadIdx.x == 0) {
-    double c0 = 1.0, c1 = 1.0;
-    ser[2 * (MS + 1)] = 1.0;
-    ser[3 * (MS + 1)] = 1.0;
-    for (int m = 1; m <= MS; ++m) {
-      c0 = c0 * (obj.beta - (m - 1)) / m;
-      c1 = c1 * (obj.beta - 1 - (m - 1)) / m;
-      ser[2 * (MS + 1) + m] = c0;
-      ser[3 * (MS + 1) + m] = c1;
-    }
-  }
-  __syncthreads();
-  PH_T(tk1);
-  while (!accepted) {
-    if (series && lam * rho <= kSeriesRho) {
-      // closed-form trial: no pass over the image
-      double s0 = 0.0, s1 = 0.0, lm = 1.0;
-      for (int m = 0; m <= MS; ++m) {
-        s0 += ser[2 * (MS + 1) + m] * lm * ser[m];
-        s1 += ser[3 * (MS + 1) + m] * lm * ser[MS + 1 + m];
-        lm *= lam;
-      }
-      const double fk =
-          obj.combine(konst, obj.c1 * s0, (MODE == 4 ? 1.0 : obj.c2) * s1, flux, (double)N);
-      ++nls;
-      ++series_evals;
-      if (fk <= fr + P.gamma * lam * gd || lam < 1e-12) {
-        f_acc = fk;
-        accepted = true;
-        break;
-      }
-      lam = lam * P.beta;
-      if (nls > ls_cap) {
-        status = 1;
-        break;
-      }
-      continue;
-    }
-    // ---- direct pass: K trial lambdas streamed over (x_tf, d_tf, gn)
-    double lamk[K];
-    lamk[0] = lam;
-#pragma unroll
-    for (int k = 1; k < K; ++k) lamk[k] = lamk[k - 1] * P.beta;
-    double t[NT];
-#pragma unroll
-    for (int k = 0; k < NT; ++k) t[k] = 0.0;
-    auto eval_px = [&](double x0, double dt, double g, double bkv) __attribute__((always_inline)) {
-      if constexpr (adapt) t[2 * K] += obj.konst(g);
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const double xt = x0 + lamk[k] * dt;
-        const double den = xt + bkv;
-        obj.template terms_m<MODE>(xt, den, g, &t[2 * k]);
-      }
-      if constexpr (K == 1 && adapt)
-        t[2 * K + 1] += beta_deriv_px(x0 + lamk[0] * dt + bkv, g, obj.beta);
-    };
-    const double* xtf = B.xtf;
-    const double* dtf = B.dtf;
-    const double* gns = B.gns;
-    const double* bks = B.bks;
-    stream2<2>(
-        Pt, npair,
-        [&](int p) {
-          struct V {
-            double2 x, d, g, b;
-          } v;
-          v.x = ld2(xtf, p);
-          v.d = ld2(dtf, p);
-          if (g32) {  // the pair's two f32 in the first f64 slot
-            v.g.x = __longlong_as_double(reinterpret_cast<const long long*>(gnf)[p]);
-            v.g.y = 0.0;
-          } else {
-            v.g = ld2(gns, p);
-          }
-          v.b = bmap ? ld2(bks, p) : double2{bks_scalar, bks_scalar};
-          return v;
-        },
-        [&](int p, const auto& v) {
-          double g0 = v.g.x, g1 = v.g.y;
-          if (g32) {
-            const long long w = __double_as_longlong(v.g.x);
-            g0 = gdec1(__int_as_float((int)(w & 0xffffffffLL)));
-            g1 = gdec1(__int_as_float((int)(w >> 32)));
-          }
-          eval_px(v.x.x, v.d.x, g0, v.b.x);
-          if (!odd || 2 * p + 1 < N) eval_px(v.x.y, v.d.y, g1, v.b.y);
-        });
-    team_sum<NT>(t, red, tm);
-    if (adapt) konst = t[2 * K];
-    ++passes;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (!accepted) {
-        const double fk = obj.combine(konst, t[2 * k], t[2 * k + 1], flux, (double)N);
-        ++nls;
-        if (fk <= fr + P.gamma * lamk[k] * gd || lamk[k] < 1e-12) {
-          accepted = true;
-          f_acc = fk;
-          lam = lamk[k];
-        }
-      }
-    }
-    if (accepted) break;
-    lam = lamk[K - 1] * P.beta;
-    if (adapt) {  // sgp.py:798-800: beta -= lr * mean(dDiv/dbeta)   (K == 1 here)
-      const double bgrad = (obj.beta == 0.0 || obj.beta == 1.0) ? 0.0 : t[2 * K + 1] / N;
-      obj.set_beta(obj.beta - lr_st * bgrad);
-    }
-    if (nls > ls_cap) {  // only for beta outside (0, 1): the reference never terminates
-      status = 1;
-      break;
-    }
-  }
-  PH_ADD(5, tk1);
-  PH_T(tk2);
-  // accept: x_tf += lam*d_tf; w = gn/den or gn*den^(b-2) (sgp.py:337-345, 790)
-  const double lam_acc = lam;
-  struct AcIn {
-    double x, d, g, bkv;
-  };
-  row_fwd2<2, true, BSGP_LS_COMP, COOP>(
-      G, Pt, G.H, G.W, G.H, B.spec, lds,
-      [&](int r, int j) {
-        const int i = r * G.W + j;
-        AcIn q;
-        q.x = B.xtf[i];
-        q.d = B.dtf[i];
-        q.g = gload(i);
-        q.bkv = bmap ? B.bks[i] : bks_scalar;
-        return q;
-      },
-      [&](int r, int j, const AcIn& q) {
-        const int i = r * G.W + j;
-        const double xt = q.x + lam_acc * q.d;
-        B.xtf[i] = xt;
-        const double den = xt + q.bkv;
-        const double g = gdec(q.g);
-        if (P.variant != BSGP_VARIANT_BETA) return g / den;  // KL: w = gn/den
-        const double p = fpow(den, obj.beta - 1);
-        B.pw[i] = p;
-        return g * (p / den);
-      });
-  PH_ADD(6, tk2);
-  if ((BSGP_FUSE_COL & 2) && (A.fuse_col & 2)) {  // T == 1: AT's column pass follows here
-    PH_T(tc0);
-    team_sync(tm);
-    col_conv<COOP>(G, Pt, B.spec, tf_of(G, img, 1), lds);
-    PH_ADD(3, tc0);
-  }
-  PH_ADD(7, tk0);
-  team_end(st, tm);
-  if (leader(tm)) {
-    if (A.out.flags)
-      A.out.flags[(size_t)img * (P.MAXIT + 1) + st.iter] = (f_acc >= fr) ? 1 : 0;
-    st.fv = f_acc;
-    st.beta = obj.beta;
-    st.konst = konst;
-    st.lam = lam_acc;
-    st.E_ls += nls;
-    st.ls_passes += passes;
-    st.ls_series += series_evals;
-    st.status |= status;
-  }
-}
-
-// ------------------------------ kernel: gradient, x update, BB, stop rules
-// sgp.py:337-414 (= 785-879): g_new = g1(den) - AT(w), x += lam*d, the
-// Barzilai-Borwein step lengths with the tau alternation, the stop rules,
-// and the outputs once the image stops (sgp.py:424-438).
-template <bool COOP>
-__global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
-  BSGP_LDS_VIEWS(A);
-  const int img = team_img(A);
-  ImgState& st = A.st[img];
-  if (st.stop) return;
-  PH_T(tk0);
-  Team tm = make_team(A, img, st);
-  const Geo& G = A.g;
-  const Part Pt = make_part(tm, G.nfw, G.W);
-  load_tw_lds(G);
-  const bsgp_params& P = A.prm;
-  const int N = G.H * G.W;
-  const int tid = threadIdx.x;
-  const bool beta_obj = P.variant == BSGP_VARIANT_BETA;
-  Bufs B = slot_bufs(A, img, st.par);
-  Dir D = make_dir(A, st);
-  const double lam = st.lam;
-  const double lo = st.lo, hi = st.hi;
-  // every state value the members use is read before the first team barrier:
-  // member 0 rewrites the state after the last one
-  const double alpha = st.alpha;
-  double vmin_ring = INFINITY;  // min(Valpha[0 .. M_alpha-2])
-  for (int k = 0; k < P.M_alpha - 1; ++k) vmin_ring = k ? py_min2(vmin_ring, st.Valpha[k]) : st.Valpha[0];
-  const int iter = st.iter;
-  const double tau0 = st.tau, init_lr = st.init_lr, lr0 = st.lr;
-  const int epoch = st.epoch;
-  const double fv = st.fv, Dcoeff = st.Dcoeff, tol = st.tol, fold_last = st.Fold[P.M - 1];
-  const double sc = st.sc;
-  double bb[6] = {0, 0, 0, 0, 0, 0};  // bk, ck, sk2.sk2, yk2.yk2, sk.sk, x.x
-  struct BbIn {
-    double p, x, g;
-  };
-  row_inv2<BSGP_BB_PRE, BSGP_BB_JCH, BSGP_BB_COMP, COOP>(
-      G, Pt, B.spec, lds,
-      [&](int r, int j) {
-        const int i = r * G.W + j;
-        BbIn q;
-        q.p = beta_obj ? B.pw[i] : 1.0;
-        q.x = B.xa[i];
-        q.g = B.ga[i];
-        return q;
-      },
-      [&](int r, int j, double at, const BbIn& q) {
-    const int i = r * G.W + j;
-    const double gnew = q.p - at;  // sgp.py:342 / 790
-    const double x = q.x, g = q.g;
-    const double d = D.d(x, g);
-    const double sk = lam * d;
-    const double xn = x + lam * d;
-    const double yk = gnew - g;
-    const double X = clipX(xn, lo, hi);
-    const double Dd = 1 / X;
-    const double sk2 = sk * Dd;
-    const double yk2 = yk * X;
-    bb[0] += sk2 * yk;
-    bb[1] += yk2 * sk;
-    bb[2] += sk2 * sk2;
-    bb[3] += yk2 * yk2;
-    bb[4] += sk * sk;
-    bb[5] += xn * xn;
-    B.xb[i] = xn;
-    B.gb[i] = gnew;
-  });
-  team_sum<6>(bb, red, tm);
-  PH_ADD(8, tk0);
-  // Barzilai-Borwein (sgp.py:366-386)
-  double alpha1, alpha2;
-  if (bb[0] <= 0) {
-    alpha1 = py_min2(10 * alpha, P.alpha_max);
-  } else {
-    alpha1 = py_min2(P.alpha_max, py_max2(P.alpha_min, bb[2] / bb[0]));
-  }
-  if (bb[1] <= 0) {
-    alpha2 = py_min2(10 * alpha, P.alpha_max);
-  } else {
-    alpha2 = py_min2(P.alpha_max, py_max2(P.alpha_min, bb[1] / bb[3]));
-  }
-  const double vmin = P.M_alpha > 1 ? py_min2(vmin_ring, alpha2) : alpha2;  // python min(Valpha)
-  double tau = tau0, anew;
-  if (iter <= 20) {
-    anew = vmin;
-  } else if (alpha2 / alpha1 < tau) {
-    anew = vmin;
-    tau = tau * 0.9;
-  } else {
-    anew = alpha1;
-    tau = tau * 1.1;
-  }
-  const double lr = (P.variant == BSGP_VARIANT_BETA && P.schedule_lr)
-                        ? init_lr * exp(-P.lr_exp_param * epoch)
-                        : lr0;
-  // stop rules (sgp.py:390-414)
-  const int it2 = iter + 1;
-  bool loop = true;
-  double crit = 0.0;
-  const double dk = Dcoeff * fv;
-  if (P.stop_criterion == 2) {
-    crit = bb[4] / bb[5];
-    loop = crit > tol;
-  } else if (P.stop_criterion == 3) {
-    crit = (fold_last - fv) / fv;
-    loop = crit > tol && crit >= 0;
-  } else if (P.stop_criterion == 4) {
-    crit = dk;
-    loop = dk > tol;
-  }
-  if (it2 > P.MAXIT) loop = false;
-  if (!loop) {
-    // outputs: x reverts to prev_x = xa (sgp.py:424-438, 892-895)
-    double* xo = A.out.x + (size_t)img * N;
-    for (int i = Pt.gt0 + tid; i < N; i += Pt.gts) xo[i] = B.xa[i] * sc;
-  }
-  team_end(st, tm);
-  if (leader(tm)) {
-    const size_t M1 = (size_t)P.MAXIT + 1;
-    A.out.discr[img * M1 + it2 - 1] = dk;
-    if (A.out.times) A.out.times[img * M1 + it2 - 1] = realtime_s() - st.t0;
-    if (A.out.crit) A.out.crit[img * M1 + it2 - 1] = crit;
-    st.Valpha[P.M_alpha - 1] = alpha2;
-    st.alpha = anew;
-    st.tau = tau;
-    st.lr = lr;
-    st.iter = it2;
-    if (loop) {
-      st.par ^= 1;
-      st.Xones = 0;
-    } else {
-      st.stop = 1;
-      A.out.iters[img] = it2 - 1;
-      if (A.out.beta_final) A.out.beta_final[img] = st.beta;
-      if (A.out.counters) {
-        int64_t* c = A.out.counters + (size_t)img * 8;
-        c[0] = st.E_p;
-        c[1] = st.E_ls;
-        c[2] = st.ls_passes;
-        c[3] = st.status |
-               ((A.tfail && __hip_atomic_load(A.tfail, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT)) ? 4 : 0);
-        c[4] = st.ls_series;
-        c[5] = tm.T;
-        c[6] = st.proj_passes;
-        c[7] = st.proj_list;
-      }
-      atomicSub(A.active, 1);
-    }
-  }
-}
-
-// ---------------------------------------- kernel: per-iteration tracking
-// errflag / save (sgp.py:240-257, 394-396, 416-422): launched after setup
-// (it = 0) and after iteration it; for every image whose iteration `it` ran it
-// writes the relative error of the scaled iterate against obj/scaling and a
-// copy of the iterate (after the update, before any revert).  Off the hot
-// kernels: only solves that ask for err / x_iter launch it.
-__global__ void __launch_bounds__(kBlock) k_track(SolveArgs A, int it) {
-  __shared__ double red[(kWaves + 1) * kMaxRed];
-  const int img = A.img0 + (int)blockIdx.x;
-  const ImgState& st = A.st[img];
-  if (it > 0 && st.iter != it + 1) return;  // iteration `it` did not run for this image
-  const int N = A.g.H * A.g.W;
-  const Bufs B = slot_bufs(A, img, st.par);
-  // k_bb flips `par` when the image goes on; a stopping image keeps it
-  const double* x = (it == 0 || !st.stop) ? B.xa : B.xb;
-  const int tid = threadIdx.x;
-  if (A.out.err) {
-    const double* o = A.in.obj + (size_t)img * N;
-    double s[2] = {0.0, 0.0};
-    for (int i = tid; i < N; i += kBlock) {
-      const double ov = o[i] / st.sc;  // obj / scaling (sgp.py:243)
-      const double e = x[i] - ov;
-      s[0] += e * e;
-      s[1] += ov * ov;
-    }
-    block_sum<2>(s, red);
-    if (tid == 0) A.out.err[(size_t)img * (A.prm.MAXIT + 1) + it] = sqrt(s[0] / s[1]);
-  }
-  if (A.out.x_iter && it > 0) {
-    double* d = A.out.x_iter + ((size_t)img * A.prm.MAXIT + (it - 1)) * N;
-    for (int i = tid; i < N; i += kBlock) d[i] = x[i];
-  }
 }
 
 // --------------------------------------------------------- TF construction
@@ -1577,75 +254,19 @@ __global__ void grad_parts_kernel(int64_t n, const double* den, const double* gn
 // Kernels come in two builds: per-wave transforms (COOP = false) and, for long
 // rows/columns (Geo::coop), workgroup-cooperative ones; separate instantiations
 // keep each build's register allocation its own.
-template <bool COOP>
-static void launch_setup_t(const SolveArgs& a, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL((k_setup<COOP>), dim3(a.nimg * a.T), dim3(kBlock), lds, s, a);
-}
+// ----------------------------------------------------------- launchers
 hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s) {
-  if (a.g.coop)
-    launch_setup_t<true>(a, lds, s);
-  else
-    launch_setup_t<false>(a, lds, s);
-  return hipGetLastError();
-}
-template <bool COOP>
-static void launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipStream_t s,
-                               hipEvent_t* ev) {
-  const dim3 grid(a.nimg * a.T), gcol(a.nimg * a.Tc), block(kBlock);
-  // ev (profiled solves): recorded before k_dir and after every kernel class
-  // (dir, col of A, ls, col of AT, bb); a class not launched gets an empty span
-  if (ev) (void)hipEventRecord(ev[0], s);
-  hipLaunchKernelGGL((k_dir<COOP>), grid, block, lds, s, a);
-  if (ev) (void)hipEventRecord(ev[1], s);
-  if (!(a.fuse_col & 5)) hipLaunchKernelGGL((k_col<COOP>), gcol, block, lds, s, a, 0);
-  if (ev) (void)hipEventRecord(ev[2], s);
-  // line-search kernel specialised on trial width, objective mode, adaptivity
-  const bsgp_params& P = a.prm;
-  const bool adapt = P.adapt_beta && P.variant == BSGP_VARIANT_BETA;
-  const bool special = a.in.beta0 ? !P.beta0_general : (P.betaParam == 0.0 || P.betaParam == 1.0);
-  const int mode = P.variant == BSGP_VARIANT_KL ? 0 : special ? -1 : P.gn_f32 ? 4 : 3;
-  if (COOP && K > 2) K = 2;  // cooperative builds carry trial widths 1 and 2
-  if (mode == 4 && K > 2) K = 2;
-  if (adapt) {
-    hipLaunchKernelGGL((k_ls<1, -1, true, COOP>), grid, block, lds, s, a);
-  } else if (mode == 0) {
-    switch (K) {
-      case 1: hipLaunchKernelGGL((k_ls<1, 0, false, COOP>), grid, block, lds, s, a); break;
-      case 2: hipLaunchKernelGGL((k_ls<2, 0, false, COOP>), grid, block, lds, s, a); break;
-      case 4: hipLaunchKernelGGL((k_ls<4, 0, false, false>), grid, block, lds, s, a); break;
-      default: hipLaunchKernelGGL((k_ls<8, 0, false, false>), grid, block, lds, s, a); break;
-    }
-  } else if (mode == 3) {
-    switch (K) {
-      case 1: hipLaunchKernelGGL((k_ls<1, 3, false, COOP>), grid, block, lds, s, a); break;
-      case 2: hipLaunchKernelGGL((k_ls<2, 3, false, COOP>), grid, block, lds, s, a); break;
-      case 4: hipLaunchKernelGGL((k_ls<4, 3, false, false>), grid, block, lds, s, a); break;
-      default: hipLaunchKernelGGL((k_ls<8, 3, false, false>), grid, block, lds, s, a); break;
-    }
-  } else if (mode == 4) {
-    if (K == 1)
-      hipLaunchKernelGGL((k_ls<1, 4, false, COOP>), grid, block, lds, s, a);
-    else
-      hipLaunchKernelGGL((k_ls<2, 4, false, COOP>), grid, block, lds, s, a);
-  } else {
-    hipLaunchKernelGGL((k_ls<2, -1, false, COOP>), grid, block, lds, s, a);
-  }
-  if (ev) (void)hipEventRecord(ev[3], s);
-  if (!(a.fuse_col & 2)) hipLaunchKernelGGL((k_col<COOP>), gcol, block, lds, s, a, 1);
-  if (ev) (void)hipEventRecord(ev[4], s);
-  hipLaunchKernelGGL((k_bb<COOP>), grid, block, lds, s, a);
-  if (ev) (void)hipEventRecord(ev[5], s);
+  if (a.storage == BSGP_STORAGE_F32) return launch_setup_f32(a, lds, s);
+  return a.g.coop ? launch_setup_t<true, double>(a, lds, s) : launch_setup_t<false, double>(a, lds, s);
 }
 hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s, hipEvent_t* ev) {
-  if (a.g.coop)
-    launch_iteration_t<true>(a, K, lds, s, ev);
-  else
-    launch_iteration_t<false>(a, K, lds, s, ev);
-  return hipGetLastError();
+  if (a.storage == BSGP_STORAGE_F32) return launch_iteration_f32(a, K, lds, s, ev);
+  return a.g.coop ? launch_iteration_t<true, double>(a, K, lds, s, ev)
+                  : launch_iteration_t<false, double>(a, K, lds, s, ev);
 }
 hipError_t launch_track(const SolveArgs& a, int it, hipStream_t s) {
-  hipLaunchKernelGGL(k_track, dim3(a.nimg), dim3(kBlock), 0, s, a, it);
-  return hipGetLastError();
+  if (a.storage == BSGP_STORAGE_F32) return launch_track_f32(a, it, s);
+  return launch_track_t<double>(a, it, s);
 }
 hipError_t launch_build_tf(const Geo& g, const double* kc, cd* spec, cd* tf, double scale,
                            int conj, size_t lds, hipStream_t s) {
@@ -1740,41 +361,17 @@ hipError_t launch_grad_parts(int64_t n, const double* den, const double* gn, dou
   return hipGetLastError();
 }
 hipError_t set_solver_lds_limit(size_t bytes) {
-  const void* fns[] = {(const void*)k_setup<false>,
-                       (const void*)k_dir<false>,
-                       (const void*)k_col<false>,
-                       (const void*)k_ls<1, -1, true, false>,
-                       (const void*)k_ls<1, 0, false, false>,
-                       (const void*)k_ls<2, 0, false, false>,
-                       (const void*)k_ls<4, 0, false, false>,
-                       (const void*)k_ls<8, 0, false, false>,
-                       (const void*)k_ls<1, 3, false, false>,
-                       (const void*)k_ls<2, 3, false, false>,
-                       (const void*)k_ls<4, 3, false, false>,
-                       (const void*)k_ls<8, 3, false, false>,
-                       (const void*)k_ls<2, -1, false, false>,
-                       (const void*)k_ls<1, 4, false, false>,
-                       (const void*)k_ls<2, 4, false, false>,
-                       (const void*)k_ls<1, 4, false, true>,
-                       (const void*)k_ls<2, 4, false, true>,
-                       (const void*)k_bb<false>,
-                       (const void*)apply_op_kernel<false>,
-                       (const void*)k_setup<true>,
-                       (const void*)k_dir<true>,
-                       (const void*)k_col<true>,
-                       (const void*)k_ls<1, -1, true, true>,
-                       (const void*)k_ls<1, 0, false, true>,
-                       (const void*)k_ls<2, 0, false, true>,
-                       (const void*)k_ls<1, 3, false, true>,
-                       (const void*)k_ls<2, 3, false, true>,
-                       (const void*)k_ls<2, -1, false, true>,
-                       (const void*)k_bb<true>,
-                       (const void*)apply_op_kernel<true>,
-                       (const void*)tf_rows_kernel<false>, (const void*)tf_rows_kernel<true>,
-                       (const void*)tf_cols_kernel<false>, (const void*)tf_cols_kernel<true>,
-                       (const void*)op_rows_kernel<false>, (const void*)op_rows_kernel<true>,
-                       (const void*)op_cols_kernel<false>, (const void*)op_cols_kernel<true>,
-                       (const void*)op_rows_inv_kernel<false>, (const void*)op_rows_inv_kernel<true>};
+  std::vector<const void*> fns = {
+      (const void*)k_col<false>, (const void*)k_col<true>,
+      (const void*)apply_op_kernel<false>, (const void*)apply_op_kernel<true>,
+      (const void*)tf_rows_kernel<false>, (const void*)tf_rows_kernel<true>,
+      (const void*)tf_cols_kernel<false>, (const void*)tf_cols_kernel<true>,
+      (const void*)op_rows_kernel<false>, (const void*)op_rows_kernel<true>,
+      (const void*)op_cols_kernel<false>, (const void*)op_cols_kernel<true>,
+      (const void*)op_rows_inv_kernel<false>, (const void*)op_rows_inv_kernel<true>};
+  solver_kernels<false, double>(fns);
+  solver_kernels<true, double>(fns);
+  solver_kernels_f32(fns);
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return e;

@@ -454,7 +454,7 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
                  use_original_SGP_Afunction=True, adapt_beta=False, betaParam=1.005, lr=1e-3,
                  lr_exp_param=0.1, schedule_lr=False, ls_spec=None, ls_series=None,
                  streams=None, team=None, proj_cache=None, gn_compact=None,
-                 device_out=False, profile=False):
+                 device_out=False, profile=False, storage="f64"):
     torch = _B.torch
     per_image = (psf.dim() if torch.is_tensor(psf) else np.ndim(psf)) == 3
     if not per_image:
@@ -487,9 +487,9 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
     if per_image:  # psf [B, kh, kw]: image i uses psf[i] (each checked as sgp.py:97-102)
         if len(psf) != Bn:
             raise ValueError("one PSF per image: psf must be [B, kh, kw]")
-        plan = _B.per_image_plan(H, W, psf, mode)
+        plan = _B.per_image_plan(H, W, psf, mode, storage=storage)
     else:
-        plan = _B.get_plan(H, W, np.asarray(psf), mode)
+        plan = _B.get_plan(H, W, np.asarray(psf), mode, storage=storage)
     out = plan.solve(gns, bkgs, prm, flux=fl, x0=x0, beta0=b0, profile=profile)
     if device_out:
         return out
@@ -567,7 +567,10 @@ def sgp_batch(gns, psf, bkgs, devices=None, **kw):
     [B, kh, kw] (a PSF per image).  Returns a dict of arrays:
     x [B,H,W], iters [B], discr [B,MAXIT+1], times, crit, flags, counters.
     ``devices=[0, 1, ...]`` shards the batch over those GPUs (contiguous
-    shards, one host thread per GPU, results concatenated in batch order)."""
+    shards, one host thread per GPU, results concatenated in batch order).
+    ``storage='f32'`` keeps the iteration vectors in float32 in HBM (every sum
+    and scalar stays float64; SURVEY config C4); the default 'f64' is the
+    reference's arithmetic."""
     if devices is not None:
         return _solve_sharded(_B.BSGP_VARIANT_KL, gns, psf, bkgs, devices, **kw)
     return _solve_batch(_B.BSGP_VARIANT_KL, gns, psf, bkgs, **kw)

@@ -410,3 +410,42 @@ def test_profiled_solve_reports_every_kernel_class(sgpmod):
     it = int(kw["MAXIT"])
     assert list(b["launches"]) == [1, it, it, it, it]  # setup, dir, col (A), ls (+AT), bb
     assert np.all(b["kernel_ms"] > 0)
+
+
+# ------------------------------------------------------- float32 storage (C4)
+def test_f32_storage_batch_within_1e3_of_reference(sgpmod):
+    """storage='f32' (iteration vectors in float32 in HBM, float64 sums and
+    scalars): the reference's lin256_beta run (SURVEY §8d C4 row tolerance,
+    1e-3 for <= 20 iterations) for single-workgroup and team solves."""
+    fx = golden("ref_lin256_beta.npz")
+    kw = ref_kwargs(fx)
+    gns = np.stack([fx["gn"].astype(np.float64)] * 3)
+    for team in (1, 8):
+        out = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, storage="f32", team=team, **kw)
+        for i in range(3):
+            assert int(out["iters"][i]) == int(fx["iters"])
+            assert rel(out["x"][i], fx["x"]) < 1e-3, (team, rel(out["x"][i], fx["x"]))
+            np.testing.assert_allclose(out["discr"][i, :11], fx["discr"], rtol=1e-3)
+            assert abs(out["x"][i].sum() - np.sum(gns[i] - 100.0)) <= 1e-6 * np.sum(gns[i])
+
+
+def test_c4_field_2048_f32_storage(sgpmod):
+    """BASELINE config C4 (2048x2048, 64x64 PSF embedded, circular A, beta-SGP)
+    with float32 storage: against the float64 oracle (5 iterations) and the
+    float64 engine (20 iterations) at 1e-3."""
+    import cpu_bench
+    import sgp_oracle
+    gn, psf = cpu_bench.make_stamp(0, 2048, 64, 5000, circular=True)
+    kw = dict(init_recon=2, proj_type=1, stop_criterion=1, alpha=10.0, ccd_sat_level=65000.0,
+              use_original_SGP_Afunction=True, schedule_lr=True, adapt_beta=False, betaParams=1.05)
+    okw = {k: v for k, v in kw.items() if k != "betaParams"}
+    xr, itr, dr, _, _ = sgp_oracle.sgp_betaDiv(gn, psf, np.float64(100.0), MAXIT=5, betaParam=1.05,
+                                               **okw)
+    o32 = sgpmod.sgp_betaDiv_batch(gn[None], psf, 100.0, storage="f32", MAXIT=5, **kw)
+    assert int(o32["iters"][0]) == itr
+    assert rel(o32["x"][0], xr) < 1e-3, rel(o32["x"][0], xr)
+    np.testing.assert_allclose(o32["discr"][0], dr, rtol=1e-3)
+    a = sgpmod.sgp_betaDiv_batch(gn[None], psf, 100.0, storage="f32", MAXIT=20, **kw)
+    b = sgpmod.sgp_betaDiv_batch(gn[None], psf, 100.0, storage="f64", MAXIT=20, **kw)
+    assert rel(a["x"][0], b["x"][0]) < 1e-3, rel(a["x"][0], b["x"][0])
+    np.testing.assert_allclose(a["discr"][0], b["discr"][0], rtol=1e-3)
