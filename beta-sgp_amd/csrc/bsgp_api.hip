@@ -124,6 +124,7 @@ struct bsgp_plan_s {
   size_t lds_fft_bytes = 0;
   size_t lds_bytes = 0;
   int wg_per_cu = 1;
+  int resident_per_cu = 1;  // workgroups of every team kernel one CU holds at once
   int ncu = 256;
   // solver workspace
   double* ws = nullptr;
@@ -199,23 +200,22 @@ static int ensure_ws(bsgp_plan p, size_t slots) {
 }
 
 // Workgroups per image.  Every member of every team must be resident at once
-// (the team barriers spin), so B*T <= CUs: one workgroup per CU always fits.
-// Each member keeps at least one row pair and one column per FFT wave.
+// (the team barriers spin): B*T never exceeds the CUs times the workgroups per
+// CU the runtime reports for every team kernel of the plan's build
+// (p->resident_per_cu, hipOccupancyMaxActiveBlocksPerMultiprocessor).  Each
+// member keeps at least one row pair and one column per FFT wave.
 static int choose_team(const bsgp_plan_s* p, int B, int req) {
   if (req == 1) return 1;
   const Geo& g = p->g;
   const int rows2 = (g.H + 1) / 2;
   int tgeo = rows2 / g.nfw;
   if (g.Qh / g.nfw < tgeo) tgeo = g.Qh / g.nfw;
-  // (cooperative plans would fit two workgroups per CU, but one per CU measured
-  // faster on C4: 1262 vs 1180 it/s)
-  int cap = p->ncu / B;
-  int T = cap < tgeo ? cap : tgeo;
-  if (req > 1) {  // explicit request: up to what stays resident (members spin on each other)
-    const int res = p->ncu * p->wg_per_cu / B;
-    T = req < tgeo ? req : tgeo;
-    if (T > res) T = res;
-  }
+  const int res = p->ncu * p->resident_per_cu / B;  // resident members per image
+  // auto: one workgroup per CU (cooperative plans would fit two per CU, but
+  // one per CU measured faster on C4: 1262 vs 1180 it/s)
+  int T = std::min(p->ncu / B, tgeo);
+  if (req > 1) T = std::min(req, tgeo);
+  T = std::min(T, res);
   return T < 1 ? 1 : T;
 }
 
@@ -375,6 +375,12 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   if (set_solver_lds_limit(p->lds_bytes) != hipSuccess) {
     delete p;
     return fail(BSGP_ERR_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+  }
+  if (team_resident_per_cu(g.coop != 0, storage, p->lds_bytes, &p->resident_per_cu) !=
+          hipSuccess ||
+      p->resident_per_cu < 1) {
+    delete p;
+    return fail(BSGP_ERR_HIP, "occupancy query of the team kernels failed");
   }
   // twiddles
   {

@@ -105,6 +105,8 @@ hipError_t launch_beta_div_deriv(int64_t n, const double* y, const double* x, do
 hipError_t launch_grad_parts(int64_t n, const double* den, const double* gn, double beta,
                              double* pow1, double* w, hipStream_t s);
 hipError_t set_solver_lds_limit(size_t bytes);
+// workgroups of every team kernel of a build (coop, storage) one CU holds at once
+hipError_t team_resident_per_cu(bool coop, int storage, size_t lds, int* per_cu);
 hipError_t launch_extract_tiles(const double* img, int W, const int* boxes, int n, int th, int tw,
                                 double* out, hipStream_t s);
 hipError_t launch_coadd_tiles(const double* tiles, int n, int th, int tw, const int* boxes, int H,

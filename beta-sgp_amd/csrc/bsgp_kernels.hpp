@@ -1384,10 +1384,24 @@ inline const void* ls_kernel(int K, int mode, bool adapt) {
   return K == 1 ? (const void*)k_ls<1, 3, false, COOP, V> : (const void*)k_ls<2, 3, false, COOP, V>;
 }
 
+// Team kernels (T > 1 workgroups per image spin on each other) need every
+// workgroup of the grid resident at once.  choose_team (bsgp_api.hip) sizes
+// teams from the occupancy the runtime reports for every team kernel of the
+// plan's build (team_resident_per_cu), so the grid fits the idle device; the
+// barrier's bounded spin turns a violation (another tenant holding CUs) into
+// status bit 4 instead of a hang.  BSGP_COOP_LAUNCH=1 launches them
+// cooperatively instead, which the runtime guarantees but which costs ~17 us
+// per launch (C2 -29 %, C4 -6 %, measured A/B).
+#ifndef BSGP_COOP_LAUNCH
+#define BSGP_COOP_LAUNCH 0
+#endif
 inline hipError_t launch_fn(const void* f, dim3 grid, size_t lds, hipStream_t s, const SolveArgs& a) {
   void* args[] = {const_cast<SolveArgs*>(&a)};
+  if (BSGP_COOP_LAUNCH && a.T > 1)
+    return hipLaunchCooperativeKernel(f, grid, dim3(kBlock), args, (unsigned)lds, s);
   return hipLaunchKernel(f, grid, dim3(kBlock), args, lds, s);
 }
+// k_col (no barrier: a team image's columns are independent)
 inline hipError_t launch_fn(const void* f, dim3 grid, size_t lds, hipStream_t s, const SolveArgs& a,
                             int i) {
   void* args[] = {const_cast<SolveArgs*>(&a), &i};
@@ -1441,11 +1455,26 @@ inline void solver_kernels(std::vector<const void*>& f) {
     for (int mode : {-1, 0, 3, 4})
       for (int K : {1, 2, 4, 8}) f.push_back(ls_kernel<COOP, V>(K, mode, adapt != 0));
 }
+// Workgroups of every team kernel of a build that one CU holds at once (the
+// minimum over the kernels, from hipOccupancyMaxActiveBlocksPerMultiprocessor).
+inline hipError_t team_resident(const std::vector<const void*>& fns, size_t lds, int* per_cu) {
+  int m = 1 << 30;
+  for (const void* f : fns) {
+    int n = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, kBlock, lds);
+    if (e != hipSuccess) return e;
+    if (n < m) m = n;
+  }
+  *per_cu = m;
+  return hipSuccess;
+}
+hipError_t team_resident_per_cu(bool coop, int storage, size_t lds, int* per_cu);
+
 // float32-storage builds (bsgp_solver_f32.hip)
 hipError_t launch_setup_f32(const SolveArgs& a, size_t lds, hipStream_t s);
 hipError_t launch_iteration_f32(const SolveArgs& a, int K, size_t lds, hipStream_t s,
                                 hipEvent_t* ev);
 hipError_t launch_track_f32(const SolveArgs& a, int it, hipStream_t s);
-void solver_kernels_f32(std::vector<const void*>& f);
+void solver_kernels_f32(std::vector<const void*>& f, bool coop);
 
 }  // namespace bsgp

@@ -264,6 +264,16 @@ hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s
   return a.g.coop ? launch_iteration_t<true, double>(a, K, lds, s, ev)
                   : launch_iteration_t<false, double>(a, K, lds, s, ev);
 }
+hipError_t team_resident_per_cu(bool coop, int storage, size_t lds, int* per_cu) {
+  std::vector<const void*> fns;
+  if (storage == BSGP_STORAGE_F32)
+    solver_kernels_f32(fns, coop);
+  else if (coop)
+    solver_kernels<true, double>(fns);
+  else
+    solver_kernels<false, double>(fns);
+  return team_resident(fns, lds, per_cu);
+}
 hipError_t launch_track(const SolveArgs& a, int it, hipStream_t s) {
   if (a.storage == BSGP_STORAGE_F32) return launch_track_f32(a, it, s);
   return launch_track_t<double>(a, it, s);
@@ -371,7 +381,8 @@ hipError_t set_solver_lds_limit(size_t bytes) {
       (const void*)op_rows_inv_kernel<false>, (const void*)op_rows_inv_kernel<true>};
   solver_kernels<false, double>(fns);
   solver_kernels<true, double>(fns);
-  solver_kernels_f32(fns);
+  solver_kernels_f32(fns, false);
+  solver_kernels_f32(fns, true);
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return e;

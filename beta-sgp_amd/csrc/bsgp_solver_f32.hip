@@ -20,9 +20,11 @@ hipError_t launch_iteration_f32(const SolveArgs& a, int K, size_t lds, hipStream
 hipError_t launch_track_f32(const SolveArgs& a, int it, hipStream_t s) {
   return launch_track_t<float>(a, it, s);
 }
-void solver_kernels_f32(std::vector<const void*>& f) {
-  solver_kernels<false, float>(f);
-  solver_kernels<true, float>(f);
+void solver_kernels_f32(std::vector<const void*>& f, bool coop) {
+  if (coop)
+    solver_kernels<true, float>(f);
+  else
+    solver_kernels<false, float>(f);
 }
 
 }  // namespace bsgp
