@@ -50,6 +50,15 @@ namespace bsgp {
 #ifndef BSGP_LS_ATTR
 #define BSGP_LS_ATTR __attribute__((amdgpu_waves_per_eu(COOP ? 1 : (K <= 2 ? 3 : 2))))
 #endif
+#ifndef BSGP_ACC_SERIES
+#define BSGP_ACC_SERIES 0  // den^(b-1) by the series at series-step accepts: same speed on C3 (A/B), off
+#endif
+#ifndef BSGP_LSACC_JCH
+#define BSGP_LSACC_JCH 1
+#endif
+#ifndef BSGP_LSACC_PF
+#define BSGP_LSACC_PF true
+#endif
 #ifndef BSGP_PROJ_U
 #define BSGP_PROJ_U 4
 #endif
@@ -912,6 +921,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   double f_acc = 0.0;
   int nls = 0, passes = 0, status = 0, series_evals = 0;
   bool accepted = false;
+  bool acc_series = false;  // the accepted trial came from the series (lam * max|u| <= rho)
   constexpr int NT = 2 * K + 2;  // [2k],[2k+1]: lambda_k sums; [2K]: const; [2K+1]: dDiv/dbeta
   // The lambda-independent sum (sum s*gn^b, or sum gn at beta = 1) is carried
   // in the state; with adaptive beta it changes with beta and is recomputed.
@@ -1034,6 +1044,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
       if (fk <= fr + P.gamma * lam * gd || lam < 1e-12) {
         f_acc = fk;
         accepted = true;
+        acc_series = true;
         break;
       }
       lam = lam * P.beta;
@@ -1123,10 +1134,16 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   PH_T(tk2);
   // accept: x_tf += lam*d_tf; w = gn/den or gn*den^(b-2) (sgp.py:337-345, 790)
   const double lam_acc = lam;
+  // A series step moved every den_i by a factor (1 + t_i), |t_i| = lam|u_i| <=
+  // kSeriesRho: den^(b-1) follows from the stored one as pw * (1 + t)^(b-1), the
+  // binomial series to t^MS (truncation < 1e-16 relative), ~25 VALU ops
+  // instead of a log and an exp per pixel.
+  const bool pw_series = BSGP_ACC_SERIES && acc_series && MODE >= 3;
+  const double bm1 = obj.beta - 1;
   struct AcIn {
-    double x, d, g, bkv;
+    double x, d, g, bkv, p0;
   };
-  row_fwd2<2, true, BSGP_LS_COMP, COOP>(
+  row_fwd2<BSGP_LSACC_JCH, BSGP_LSACC_PF, BSGP_LS_COMP, COOP>(
       G, Pt, G.H, G.W, G.H, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
@@ -1135,6 +1152,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
         q.d = B.dtf[i];
         q.g = gload(i);
         q.bkv = bmap ? B.bks[i] : bks_scalar;
+        q.p0 = pw_series ? (double)B.pw[i] : 0.0;
         return q;
       },
       [&](int r, int j, const AcIn& q) {
@@ -1144,7 +1162,17 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
         const double den = xt + q.bkv;
         const double g = gdec(q.g);
         if (P.variant != BSGP_VARIANT_BETA) return g / den;  // KL: w = gn/den
-        const double p = fpow(den, obj.beta - 1);
+        double p;
+        if (pw_series) {
+          const double t = lam_acc * (q.d / (q.x + q.bkv));
+          // (1+t)^(b-1) = 1 + e1 t (1 + e2 t (1 + ... (1 + e6 t))), e_m = (b-m)/m
+          double h = 1.0;
+#pragma unroll
+          for (int m = MS; m >= 1; --m) h = fma(fma(obj.beta, 1.0 / m, -1.0) * t, h, 1.0);
+          p = q.p0 * h;
+        } else {
+          p = fpow(den, bm1);
+        }
         B.pw[i] = p;
         return g * (p / den);
       });
