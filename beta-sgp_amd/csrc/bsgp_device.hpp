@@ -314,6 +314,69 @@ __device__ __forceinline__ void team_sum(double (&v)[NV], double* red, Team& t) 
   __syncthreads();
 }
 
+// NV sums and NM maxima in ONE team barrier (NaN propagates through the
+// maxima like np.max); the same values as separate team_sum / team_max calls.
+// Used where a kernel needs several reductions at the same point: the line
+// search's first pass (sums + max|u|), setup's statistics, the scaling-matrix
+// bounds (max y and -min y).
+template <int NV, int NM>
+__device__ __forceinline__ void team_reduce(double (&v)[NV > 0 ? NV : 1], double (&mx)[NM], double* red,
+                                            Team& t) {
+  static_assert(NV + NM <= kMaxRed, "too many values");
+#pragma unroll
+  for (int k = 0; k < NM; ++k) mx[k] = block_max(mx[k], red);
+  if constexpr (NV > 0) block_sum<NV>(v, red);
+  if (t.T == 1) return;
+  double* slot = t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) st_sc1(slot + (size_t)t.m * kMaxRed + i, v[i]);
+#pragma unroll
+    for (int k = 0; k < NM; ++k) st_sc1(slot + (size_t)t.m * kMaxRed + NV + k, mx[k]);
+  }
+  team_red_barrier(t);
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    double s[NV + 1], m[NM];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) s[i] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NM; ++k) m[k] = -INFINITY;
+    for (int mm = lane; mm < t.T; mm += 64) {
+      const double* q = slot + (size_t)mm * kMaxRed;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) s[i] += ld_sc1(q + i);
+#pragma unroll
+      for (int k = 0; k < NM; ++k) {
+        const double u = ld_sc1(q + NV + k);
+        m[k] = (u > m[k] || u != u) ? u : m[k];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const double r = wave_sum(s[i]);
+      if (lane == 0) red[kWaves * kMaxRed + i] = r;
+    }
+#pragma unroll
+    for (int k = 0; k < NM; ++k) {
+      const double r = wave_max(m[k]);
+      if (lane == 0) red[kWaves * kMaxRed + NV + k] = r;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = red[kWaves * kMaxRed + i];
+#pragma unroll
+  for (int k = 0; k < NM; ++k) mx[k] = red[kWaves * kMaxRed + NV + k];
+  __syncthreads();
+}
+template <int NV>
+__device__ __forceinline__ void team_sum_max(double (&v)[NV], double& mx, double* red, Team& t) {
+  double m[1] = {mx};
+  team_reduce<NV, 1>(v, m, red, t);
+  mx = m[0];
+}
+
 // Team max / min (NaN propagates, like np.max / np.min)
 template <bool MAX>
 __device__ __forceinline__ double team_ext(double v, double* red, Team& t) {
