@@ -27,6 +27,35 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kMaxRed = 24;  // doubles reduced at once
 constexpr int kSharedBytes = 512;  // LDS after the wave partials: reduced totals + scalars
 
+// Phase profile (builds with -DBSGP_PHASE_PROF only): thread 0 of every
+// workgroup adds the shader cycles it spent in each phase to g_phase[slot]
+// (tools/phase_prof.py reads them through bsgp_phase_prof).  Row passes given
+// a slot base PHS >= 0 split their time into operand batches (PHS), FFTs
+// (PHS + 1) and spectrum stores / staging (PHS + 2), as seen by wave 0.
+constexpr int kPhaseSlots = 32;
+#ifdef BSGP_PHASE_PROF
+static __device__ unsigned long long g_phase[kPhaseSlots];
+#define PH_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PH_ADD(slot, t0)                                                                 \
+  do {                                                                                   \
+    if (threadIdx.x == 0) atomicAdd(&g_phase[slot], __builtin_amdgcn_s_memtime() - (t0)); \
+  } while (0)
+#define PH_SUB(slot, t)                                                                 \
+  do {                                                                                  \
+    if (PHS >= 0) {                                                                     \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                        \
+      if (threadIdx.x == 0) atomicAdd(&g_phase[(slot) < 0 ? 0 : (slot)], t_ - (t));       \
+      t = t_;                                                                           \
+    }                                                                                   \
+  } while (0)
+#define PH_SUB_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define PH_T(v)
+#define PH_ADD(slot, t0)
+#define PH_SUB(slot, t)
+#define PH_SUB_T(v)
+#endif
+
 // Geometry of one conv plan (P x Q FFT grid, H x W image).
 struct Geo {
   int H, W;      // image
@@ -463,17 +492,19 @@ constexpr int kGCH = 3;  // stored spectrum columns per lane in one gather batch
 constexpr int kPCH = 5;  // column elements per lane in one batch (P <= 320: one batch)
 
 // Issue the loads of one batch of row pixels j0 + lane + 64u (u < kJCH) of
-// rows r and r+1.
+// rows r and r+1.  Branch-free: a lane past the row end reloads the last
+// pixel and a missing row r+1 reloads row r (the values go unused).  A load
+// under a condition would end in a join where the compiler waits for every
+// outstanding load (s_waitcnt vmcnt(0)), defeating batches kept in flight.
 template <int JCH, class LD, class V>
 __device__ __forceinline__ void load_rows(LD& ld, int r, bool two, int j0, int lane, int ncols,
                                           V (&v0)[JCH], V (&v1)[JCH]) {
+  const int r1 = two ? r + 1 : r;
 #pragma unroll
   for (int u = 0; u < JCH; ++u) {
-    const int j = j0 + lane + 64 * u;
-    if (j < ncols) {
-      v0[u] = ld(r, j);
-      if (two) v1[u] = ld(r + 1, j);
-    }
+    const int j = min(j0 + lane + 64 * u, ncols - 1);
+    v0[u] = ld(r, j);
+    v1[u] = ld(r1, j);
   }
 }
 
@@ -674,8 +705,11 @@ __device__ __forceinline__ void coop_col_conv(const Geo& G, const Part& D, cd* s
 // PF: the first operand batch of the wave's next row pair is issued before
 // the FFT of the current one (its latency hides under the FFT; the batch
 // registers stay live across it).
+// PIPE: the operand batch j0 + 64*JCH is issued before batch j0 is computed
+// (two batches in flight per wave instead of one round trip per batch; costs
+// a second set of batch registers outside the FFT).
 template <int JCH = kJCH, bool PF = false, bool COMP = BSGP_FFT_COMPOSITE, bool COOP = false,
-          class LD, class MK>
+          bool PIPE = false, int PHS = -1, class LD, class MK>
 __device__ __forceinline__ void row_fwd2(const Geo& G, const Part& D, int nrows, int ncols,
                                          int ldim, cd* spec, cd* lds, LD&& ld, MK&& mk) {
   if constexpr (COOP) {
@@ -691,33 +725,56 @@ __device__ __forceinline__ void row_fwd2(const Geo& G, const Part& D, int nrows,
     int r = 2 * (D.gw0 + w);
     V v0[JCH], v1[JCH];
     if (PF && r < nrows) load_rows<JCH>(ld, r, (r + 1) < nrows, 0, lane, ncols, v0, v1);
+    PH_SUB_T(tph);
     for (; r < nrows; r += 2 * D.gws) {
       const bool two = (r + 1) < nrows;
-      for (int j0 = 0; j0 < G.Q; j0 += 64 * JCH) {
-        if (!PF || j0 > 0) load_rows<JCH>(ld, r, two, j0, lane, ncols, v0, v1);
+      auto put = [&](int j0, const V (&w0)[JCH], const V (&w1)[JCH]) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < JCH; ++u) {
           const int j = j0 + lane + 64 * u;
           if (j < G.Q) {
             double va = 0.0, vb = 0.0;
             if (j < ncols) {
-              va = mk(r, j, v0[u]);
-              if (two) vb = mk(r + 1, j, v1[u]);
+              va = mk(r, j, w0[u]);
+              if (two) vb = mk(r + 1, j, w1[u]);
             }
             a[j] = cmk(va, vb);
           }
+        }
+      };
+      if constexpr (PIPE) {
+        constexpr int S = 64 * JCH;
+        V u0[JCH], u1[JCH];
+        if (!PF) load_rows<JCH>(ld, r, two, 0, lane, ncols, v0, v1);
+        // (loads past the row end are clamped, not skipped: a skipped load
+        // would be a branch whose join waits for every load in flight)
+        for (int j0 = 0; j0 < G.Q; j0 += 2 * S) {
+          load_rows<JCH>(ld, r, two, j0 + S, lane, ncols, u0, u1);
+          put(j0, v0, v1);
+          if (j0 + S < G.Q) {
+            load_rows<JCH>(ld, r, two, j0 + 2 * S, lane, ncols, v0, v1);
+            put(j0 + S, u0, u1);
+          }
+        }
+      } else {
+        for (int j0 = 0; j0 < G.Q; j0 += 64 * JCH) {
+          if (!PF || j0 > 0) load_rows<JCH>(ld, r, two, j0, lane, ncols, v0, v1);
+          put(j0, v0, v1);
         }
       }
       const int rn = r + 2 * D.gws;
       if (PF && rn < nrows) load_rows<JCH>(ld, rn, (rn + 1) < nrows, 0, lane, ncols, v0, v1);
       wave_sync();
+      PH_SUB(PHS, tph);
       cd* Z = fft_any<COMP>(a, b, G.fq, false, lane, 64, WaveSync());
+      PH_SUB(PHS + 1, tph);
       for (int k = lane; k < G.Qh; k += 64) {
         cd ak, bk;
         r2c_split(Z, G.Q, k, &ak, &bk);
         store_pair(spec + (size_t)k * ldim + r, two, pair_ok, ak, bk);
       }
       wave_sync();
+      PH_SUB(PHS + 2, tph);
     }
   }
 }
@@ -792,8 +849,9 @@ __device__ __forceinline__ void unpack_pair(const Geo& G, const cd* F, bool two,
 // consumer of r; the first pair is gathered through registers.
 // PRE: the first operand batch is issued before the FFT (costs its registers
 // across the FFT).
-template <bool PRE, int JCH = kJCH, bool COMP = BSGP_FFT_COMPOSITE, bool COOP = false, class LD,
-          class USE>
+// PIPE: as row_fwd2 (batch j0 + 64*JCH in flight while batch j0 is consumed).
+template <bool PRE, int JCH = kJCH, bool COMP = BSGP_FFT_COMPOSITE, bool COOP = false,
+          bool PIPE = false, int PHS = -1, class LD, class USE>
 __device__ __forceinline__ void row_inv2(const Geo& G, const Part& D, const cd* spec, cd* lds,
                                          LD&& ld, USE&& use) {
   if constexpr (COOP) {
@@ -806,29 +864,50 @@ __device__ __forceinline__ void row_inv2(const Geo& G, const Part& D, const cd* 
     cd* in = lds + w * 2 * G.lpad;
     cd* other = in + G.lpad;
     int r = 2 * (D.gw0 + w);
+    PH_SUB_T(tph);
     if (r < G.H) gather_pair(G, spec, G.H, r, (r + 1) < G.H, in, lane);
     for (; r < G.H; r += 2 * D.gws) {
       const bool two = (r + 1) < G.H;
       V v0[JCH], v1[JCH];
       if (PRE) load_rows<JCH>(ld, r, two, 0, lane, G.W, v0, v1);
       wave_sync();
+      PH_SUB(PHS + 2, tph);
       cd* Z = fft_any<COMP>(in, other, G.fq, true, lane, 64, WaveSync());
+      PH_SUB(PHS + 1, tph);
       cd* F = (Z == in) ? other : in;
       const int rn = r + 2 * D.gws;
       const bool next = rn < G.H, two_n = (rn + 1) < G.H;
       if (next) stage_pair(G, spec, G.H, rn, two_n, F, lane);
-      for (int j0 = 0; j0 < G.W; j0 += 64 * JCH) {
-        if (!PRE || j0 > 0) load_rows<JCH>(ld, r, two, j0, lane, G.W, v0, v1);
+      auto eat = [&](int j0, const V (&w0)[JCH], const V (&w1)[JCH]) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < JCH; ++u) {
           const int j = j0 + lane + 64 * u;
           if (j < G.W) {
             const cd z = Z[j];
-            use(r, j, z.x, v0[u]);
-            if (two) use(r + 1, j, z.y, v1[u]);
+            use(r, j, z.x, w0[u]);
+            if (two) use(r + 1, j, z.y, w1[u]);
           }
         }
+      };
+      if constexpr (PIPE) {
+        constexpr int S = 64 * JCH;
+        V u0[JCH], u1[JCH];
+        if (!PRE) load_rows<JCH>(ld, r, two, 0, lane, G.W, v0, v1);
+        for (int j0 = 0; j0 < G.W; j0 += 2 * S) {
+          load_rows<JCH>(ld, r, two, j0 + S, lane, G.W, u0, u1);  // clamped (see row_fwd2)
+          eat(j0, v0, v1);
+          if (j0 + S < G.W) {
+            load_rows<JCH>(ld, r, two, j0 + 2 * S, lane, G.W, v0, v1);
+            eat(j0 + S, u0, u1);
+          }
+        }
+      } else {
+        for (int j0 = 0; j0 < G.W; j0 += 64 * JCH) {
+          if (!PRE || j0 > 0) load_rows<JCH>(ld, r, two, j0, lane, G.W, v0, v1);
+          eat(j0, v0, v1);
+        }
       }
+      PH_SUB(PHS, tph);
       if (next) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // staged pair landed
         wave_sync();                                       // and Z fully consumed

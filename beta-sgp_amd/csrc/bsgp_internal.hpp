@@ -116,7 +116,6 @@ hipError_t launch_fits_to_f64(const void* raw, int64_t n, int bitpix, double bsc
 struct PsfModel;
 hipError_t launch_psf_stamps(const PsfModel& m, const double* xy, int n, int spatial,
                              int normalize, double* out, hipStream_t s);
-constexpr int kPhaseSlots = 16;
 hipError_t phase_prof(unsigned long long* out, int n, int reset);
 
 }  // namespace bsgp

@@ -59,6 +59,17 @@ namespace bsgp {
 #ifndef BSGP_LSACC_PF
 #define BSGP_LSACC_PF true
 #endif
+// two operand batches in flight in the single-column row passes (row_inv2 /
+// row_fwd2 PIPE): k_ls pass 1 and accept, k_bb
+#ifndef BSGP_LS1_PIPE
+#define BSGP_LS1_PIPE false
+#endif
+#ifndef BSGP_LSACC_PIPE
+#define BSGP_LSACC_PIPE false
+#endif
+#ifndef BSGP_BB_PIPE
+#define BSGP_BB_PIPE false
+#endif
 #ifndef BSGP_PROJ_U
 #define BSGP_PROJ_U 4
 #endif
@@ -86,20 +97,7 @@ namespace bsgp {
 #define BSGP_BB_JCH 1  // one column per operand batch: 117 VGPRs, 4 waves/SIMD (k_bb -17 %, A/B)
 #endif
 
-// Phase profile (builds with -DBSGP_PHASE_PROF only): thread 0 of every
-// workgroup adds the shader cycles it spent in each phase to g_phase[slot]
-// (tools/phase_prof.py reads them through bsgp_phase_prof).
-#ifdef BSGP_PHASE_PROF
-static __device__ unsigned long long g_phase[kPhaseSlots];
-#define PH_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define PH_ADD(slot, t0)                                                                 \
-  do {                                                                                   \
-    if (threadIdx.x == 0) atomicAdd(&g_phase[slot], __builtin_amdgcn_s_memtime() - (t0)); \
-  } while (0)
-#else
-#define PH_T(v)
-#define PH_ADD(slot, t0)
-#endif
+// (phase profile macros PH_T / PH_ADD: bsgp_device.hpp)
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ double clipX(double x, double lo, double hi) {
   // X[X < lo] = lo; X[X > hi] = hi  (sgp.py:355-357)
@@ -150,6 +148,40 @@ __device__ __forceinline__ double2 ld2(const double* a, int p) {
 __device__ __forceinline__ double2 ld2(const float* a, int p) {
   const float2 f = reinterpret_cast<const float2*>(a)[p];
   return double2{(double)f.x, (double)f.y};
+}
+
+// Branch-free optional operands.  A load under a runtime condition compiles to
+// a branch whose join waits for it (s_waitcnt vmcnt(0) before the phi copy),
+// which serialises the loads of an operand batch.  Instead every lane loads:
+// its own pixel when the wave-uniform flag is on, element 0 of the same slot
+// vector (one cache line for the whole wave) when it is off; the value is
+// selected after the load.  Every slot vector exists in every plan.
+template <class T>
+__device__ __forceinline__ double opt_ld(bool on, const T* a, int i, double off) {
+  const double v = (double)a[on ? i : 0];
+  return on ? v : off;
+}
+__device__ __forceinline__ double2 opt_ld2(bool on, const double* a, int p, double off) {
+  const double2 v = ld2(a, on ? p : 0);
+  return on ? v : double2{off, off};
+}
+// The observed-image operand in one 8-byte load for both layouts: compact
+// (ImgState::g32, the raw float32 gnf[i] in the low word) or float64 gns[i].
+// The compact array is the first half of the gns slot vector, so the word
+// after gnf[i] is in bounds.
+__device__ __forceinline__ double g_raw(bool g32, const double* gns, int i) {
+  const unsigned int* w = reinterpret_cast<const unsigned int*>(gns) + (g32 ? i : 2 * i);
+  unsigned long long u;
+  __builtin_memcpy(&u, __builtin_assume_aligned(w, 4), 8);
+  return __longlong_as_double((long long)u);
+}
+// Pixel pair p: compact = floats gnf[2p], gnf[2p+1] in the first 8 bytes
+// (16 bytes are read either way; the wave's lines are the same).
+__device__ __forceinline__ double2 g_raw2(bool g32, const double* gns, int p) {
+  const double* a = g32 ? gns + p : gns + 2 * p;  // gnf + 2p == (double*)gns + p
+  double2 v;
+  __builtin_memcpy(&v, __builtin_assume_aligned(a, 8), 16);
+  return v;
 }
 
 // Per-image slot vectors (x and g double-buffered; `par` picks the current
@@ -814,7 +846,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_DIR_ATTR k_dir(SolveArgs A) {
   PH_ADD(0, tk0);
   PH_T(tk1);
   double gd[1] = {0.0};
-  row_fwd2<BSGP_DIR_JCH, BSGP_DIR_PF, BSGP_DIR_COMP, COOP>(
+  row_fwd2<BSGP_DIR_JCH, BSGP_DIR_PF, BSGP_DIR_COMP, COOP, false, 22>(
       G, Pt, G.H, G.W, G.H, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
@@ -904,7 +936,6 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   // compact gn (ImgState::g32): loaders fetch the raw f32, users decode it
   const int g32 = st.g32;
   const double gsc = st.sc, grc = 1.0 / st.sc, gfill = st.gfill;
-  const float* gnf = reinterpret_cast<const float*>(B.gns);
   // (the raw f32 travels in the low word of the f64 operand register, so both
   // storage modes use the same registers)
   auto gdec1 = [&](float v) __attribute__((always_inline)) {
@@ -913,9 +944,6 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   };
   auto gdec = [&](double r) __attribute__((always_inline)) {
     return g32 ? gdec1(__int_as_float(__double2loint(r))) : r;
-  };
-  auto gload = [&](int i) __attribute__((always_inline)) {
-    return g32 ? __hiloint2double(0, __float_as_int(gnf[i])) : B.gns[i];
   };
   double fr = st.Fold[0];
   for (int k = 1; k < P.M; ++k) fr = py_max2(fr, st.Fold[k]);
@@ -954,15 +982,15 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
     struct LsIn {
       double x0, g, p0, bkv;
     };
-    row_inv2<BSGP_LS1_PRE, BSGP_LS1_JCH, BSGP_LS_COMP, COOP>(
+    row_inv2<BSGP_LS1_PRE, BSGP_LS1_JCH, BSGP_LS_COMP, COOP, BSGP_LS1_PIPE, 13>(
         G, Pt, B.spec, lds,
         [&](int r, int j) {
           const int i = r * G.W + j;
           LsIn q;
           q.x0 = B.xtf[i];
-          q.g = gload(i);
-          q.p0 = series ? B.pw[i] : 0.0;
-          q.bkv = bmap ? B.bks[i] : bks_scalar;
+          q.g = g_raw(g32, B.gns, i);
+          q.p0 = opt_ld(series, B.pw, i, 0.0);
+          q.bkv = opt_ld(bmap, B.bks, i, bks_scalar);
           return q;
         },
         [&](int r, int j, double v, const LsIn& q) {
@@ -1090,13 +1118,8 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
           } v;
           v.x = ld2(xtf, p);
           v.d = ld2(dtf, p);
-          if (g32) {  // the pair's two f32 in the first f64 slot
-            v.g.x = __longlong_as_double(reinterpret_cast<const long long*>(gnf)[p]);
-            v.g.y = 0.0;
-          } else {
-            v.g = ld2(gns, p);
-          }
-          v.b = bmap ? ld2(bks, p) : double2{bks_scalar, bks_scalar};
+          v.g = g_raw2(g32, gns, p);  // compact: the pair's two f32 in the first f64
+          v.b = opt_ld2(bmap, bks, p, bks_scalar);
           return v;
         },
         [&](int p, const auto& v) {
@@ -1148,16 +1171,16 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   struct AcIn {
     double x, d, g, bkv, p0;
   };
-  row_fwd2<BSGP_LSACC_JCH, BSGP_LSACC_PF, BSGP_LS_COMP, COOP>(
+  row_fwd2<BSGP_LSACC_JCH, BSGP_LSACC_PF, BSGP_LS_COMP, COOP, BSGP_LSACC_PIPE, 16>(
       G, Pt, G.H, G.W, G.H, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
         AcIn q;
         q.x = B.xtf[i];
         q.d = B.dtf[i];
-        q.g = gload(i);
-        q.bkv = bmap ? B.bks[i] : bks_scalar;
-        q.p0 = pw_series ? (double)B.pw[i] : 0.0;
+        q.g = g_raw(g32, B.gns, i);
+        q.bkv = opt_ld(bmap, B.bks, i, bks_scalar);
+        q.p0 = opt_ld(pw_series, B.pw, i, 0.0);
         return q;
       },
       [&](int r, int j, const AcIn& q) {
@@ -1241,12 +1264,12 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
   struct BbIn {
     double p, x, g;
   };
-  row_inv2<BSGP_BB_PRE, BSGP_BB_JCH, BSGP_BB_COMP, COOP>(
+  row_inv2<BSGP_BB_PRE, BSGP_BB_JCH, BSGP_BB_COMP, COOP, BSGP_BB_PIPE, 19>(
       G, Pt, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
         BbIn q;
-        q.p = beta_obj ? B.pw[i] : 1.0;
+        q.p = opt_ld(beta_obj, B.pw, i, 1.0);
         q.x = B.xa[i];
         q.g = B.ga[i];
         return q;

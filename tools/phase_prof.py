@@ -21,7 +21,11 @@ for p in (ROOT, os.path.join(ROOT, "beta-sgp_amd")):
 SLOTS = {0: "k_dir projection", 1: "k_dir row pass", 2: "k_dir total", 3: "k_col total",
          4: "k_ls pass 1 (rows of A(d))", 5: "k_ls search loop", 6: "k_ls accept rows",
          7: "k_ls total", 8: "k_bb rows + BB sums", 10: "  proj first pass",
-         11: "  proj list evals", 12: "  proj miss passes"}
+         11: "  proj list evals", 12: "  proj miss passes",
+         13: "  ls1 rows: operand batches", 14: "  ls1 rows: FFT", 15: "  ls1 rows: stage/unpack",
+         16: "  accept rows: operand batches", 17: "  accept rows: FFT", 18: "  accept rows: stores",
+         19: "  bb rows: operand batches", 20: "  bb rows: FFT", 21: "  bb rows: stage/unpack",
+         22: "  dir rows: operand batches", 23: "  dir rows: FFT", 24: "  dir rows: stores"}
 
 
 def main():
@@ -38,16 +42,16 @@ def main():
     bench.torch = torch
     L = _bsgp.lib()
     L.bsgp_phase_prof.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
-    buf = (ctypes.c_uint64 * 16)()
+    buf = (ctypes.c_uint64 * 32)()
     cfg = bench.CONFIGS[args.config]
     B = args.batch or cfg["batch"]
     gn, psf = bench.synth_batch(B, cfg["n"], cfg["k"], cfg["nstars"], 0, circular=cfg["circular"])
     bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
     kw = bench.solve_kwargs(args.maxit, None, args.streams, None, circular=cfg["circular"])
     sgp.sgp_betaDiv_batch(gn, psf, bkg, device_out=True, **kw)
-    _bsgp.check(L.bsgp_phase_prof(buf, 16, 1))  # reset after warm-up
+    _bsgp.check(L.bsgp_phase_prof(buf, 32, 1))  # reset after warm-up
     out = sgp.sgp_betaDiv_batch(gn, psf, bkg, device_out=True, **kw)
-    _bsgp.check(L.bsgp_phase_prof(buf, 16, 1))
+    _bsgp.check(L.bsgp_phase_prof(buf, 32, 1))
     n = float(out["iters"].sum().item()) * float(out["counters"][0, 5].item())  # x team size
     for k, name in SLOTS.items():
         print(f"{name:32s} {buf[k] / n:12.0f} cycles per image-iteration"
