@@ -40,7 +40,7 @@ import time
 # 8 hardware queues for this process (read by the HIP runtime when torch
 # initialises it): the solve then runs 8 sub-batches instead of 4 (+2.8 % on
 # C3).  Set before torch is imported; inherited by spawned ranks.
-os.environ["GPU_MAX_HW_QUEUES"] = "8"
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("BSGP_BENCH_HW_QUEUES", "8")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for p in (ROOT, os.path.join(ROOT, "beta-sgp_amd"), os.path.join(ROOT, "oracle")):

@@ -137,7 +137,7 @@ struct bsgp_plan_s {
   int* active = nullptr;     // device counter of images still iterating
   int* active_h = nullptr;   // pinned host mirror for polling
   // sub-batch streams: phases of different sub-batches overlap on the device
-  static constexpr int kMaxStreams = 8;
+  static constexpr int kMaxStreams = 16;
   hipStream_t sub[kMaxStreams] = {};
   hipEvent_t ev_fork = nullptr;
   hipEvent_t ev_join[kMaxStreams] = {};

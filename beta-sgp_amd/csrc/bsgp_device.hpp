@@ -1003,10 +1003,12 @@ __device__ __forceinline__ void col_conv(const Geo& G, const Part& D, cd* spec, 
         cd cv[kPCH];
 #pragma unroll
         for (int u = 0; u < kPCH; ++u) {
+          // branch-free (a conditional load ends in a join that waits for every
+          // load in flight): clamp the index, select after the load
           const int p = p0 + lane + 64 * u;
-          cv[u] = cmk(0.0, 0.0);
-          if (p < G.H) cv[u] = col[p];
-          if (one && p < G.P) tv[u] = t[p];
+          const cd c = col[min(p, G.H - 1)];
+          cv[u] = p < G.H ? c : cmk(0.0, 0.0);
+          if (one) tv[u] = t[min(p, G.P - 1)];
         }
 #pragma unroll
         for (int u = 0; u < kPCH; ++u) {
@@ -1017,6 +1019,15 @@ __device__ __forceinline__ void col_conv(const Geo& G, const Part& D, cd* spec, 
       wave_sync();
       cd* Z = fft_any(a, b, G.fp, false, lane, 64, WaveSync());
       if (one) {
+#pragma unroll
+        for (int u = 0; u < kPCH; ++u) {
+          const int p = lane + 64 * u;
+          if (p < G.P) Z[p] = cmul(Z[p], tv[u]);
+        }
+      } else if (G.P <= 64 * kPCH) {
+        // the TF column in one load batch after the FFT (one round trip)
+#pragma unroll
+        for (int u = 0; u < kPCH; ++u) tv[u] = t[min(lane + 64 * u, G.P - 1)];
 #pragma unroll
         for (int u = 0; u < kPCH; ++u) {
           const int p = lane + 64 * u;

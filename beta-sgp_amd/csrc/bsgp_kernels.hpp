@@ -118,10 +118,7 @@ __device__ __forceinline__ void stream_range(int p0, int p1, LD&& ld, CP&& cp) {
   for (int b = p0 + threadIdx.x; b < p1; b += kBlock * U) {
     T v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int p = b + u * kBlock;
-      if (p < p1) v[u] = ld(p);
-    }
+    for (int u = 0; u < U; ++u) v[u] = ld(min(b + u * kBlock, p1 - 1));  // clamped, branch-free
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int p = b + u * kBlock;

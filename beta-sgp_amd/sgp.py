@@ -67,7 +67,7 @@ def _hw_queues():
 # streams) so that kernels of different phases overlap.  One per hardware queue
 # HIP opens for the process (GPU_MAX_HW_QUEUES, 4 by default): C3 A/B with 4
 # queues: 4 > 3 > 2 sub-batches (8 collapse to 164 k); with 8 queues 8
-# sub-batches are +2.8 % over 4.
+# sub-batches are +2.8 % over 4; 16 queues with 12 or 16 sub-batches: no gain.
 STREAMS_DEFAULT = 8 if _hw_queues() >= 8 else 4
 TEAM_DEFAULT = 0  # workgroups per image: 0 = auto (spread small batches over the CUs)
 PROJ_CACHE_DEFAULT = 1  # projectDF evaluations inside a known root bracket read a pixel list

@@ -76,7 +76,7 @@ typedef struct {
   int32_t bkg_is_map;     /* bkg is [B][H][W] instead of [B] scalars               */
   int32_t ls_spec;        /* line-search lambdas evaluated per pass (1..8); 1 when adapt_beta */
   int32_t ls_series;      /* 1: small trial steps from the moment series (general beta) */
-  int32_t streams;        /* sub-batches run on this many streams (1..8: the caller's + 7 plan
+  int32_t streams;        /* sub-batches run on this many streams (1..16: the caller's + 15 plan
                              streams) so phases overlap; more than GPU_MAX_HW_QUEUES share queues */
   int32_t team;           /* workgroups cooperating on one image: 0 = auto (spread the
                              batch over the CUs when B is small), 1 = one per image,

@@ -341,7 +341,7 @@ def test_bench_c3_path_exact(sgpmod):
     gn[0] = torch.from_numpy(fx["gn"].astype(np.float64)).cuda()
     bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
     kw = bench.solve_kwargs(10, None)
-    assert kw["streams"] is None and kw["team"] is None and sgpmod.STREAMS_DEFAULT in (4, 8)
+    assert kw["streams"] is None and kw["team"] is None and sgpmod.STREAMS_DEFAULT in (4, 8, 16)
     assert sgpmod.GN_COMPACT_DEFAULT == 1
     out = sgpmod.sgp_betaDiv_batch(gn, psf, bkg, **kw)
     x = out["x"]
