@@ -444,7 +444,14 @@ __device__ __forceinline__ double team_min(double v, double* red, Team& t) {
 #define BSGP_FAST_EXP 0  // measured: ocml exp is faster at k_ls's occupancy (A/B -2 %)
 #endif
 __device__ __forceinline__ double fpow(double x, double a) {
+#ifdef BSGP_VALU_X2  // diagnostic: twice the pow work, same values
+  const double x2 = x + 0.0 * a * x;
+  const double r1 = exp(a * fast_log(x));
+  const double r2 = exp(a * fast_log(x2));
+  return r1 == r2 ? r1 : r2;
+#else
   return BSGP_FAST_EXP ? fast_exp(a * fast_log(x)) : exp(a * fast_log(x));
+#endif
 }
 
 // numpy-like max/min of two scalars (np.max([a, b]): NaN propagates)
@@ -532,12 +539,10 @@ __device__ __forceinline__ void coop_row_fwd(const Geo& G, const Part& D, int nr
     for (int j0 = 0; j0 < G.Q; j0 += kBlock * kCCH) {
       V v0[kCCH], v1[kCCH];
 #pragma unroll
-      for (int u = 0; u < kCCH; ++u) {
-        const int j = j0 + t + kBlock * u;
-        if (j < ncols) {
-          v0[u] = ld(r, j);
-          if (two) v1[u] = ld(r + 1, j);
-        }
+      for (int u = 0; u < kCCH; ++u) {  // clamped, branch-free (load_rows)
+        const int j = min(j0 + t + kBlock * u, ncols - 1);
+        v0[u] = ld(r, j);
+        v1[u] = ld(two ? r + 1 : r, j);
       }
 #pragma unroll
       for (int u = 0; u < kCCH; ++u) {
@@ -568,13 +573,12 @@ __device__ __forceinline__ void coop_gather(const Geo& G, const cd* spec, int r,
   for (int k0 = 0; k0 < G.Qh; k0 += kBlock * kCCH) {
     cd A[kCCH], B[kCCH];
 #pragma unroll
-    for (int u = 0; u < kCCH; ++u) {
-      const int k = k0 + t + kBlock * u;
-      if (k < G.Qh) {
-        const cd* col = spec + (size_t)k * G.H + r;
-        A[u] = col[0];
-        B[u] = two ? col[1] : cmk(0.0, 0.0);
-      }
+    for (int u = 0; u < kCCH; ++u) {  // clamped, branch-free
+      const int k = min(k0 + t + kBlock * u, G.Qh - 1);
+      const cd* col = spec + (size_t)k * G.H + r;
+      A[u] = col[0];
+      const cd b = col[two ? 1 : 0];
+      B[u] = two ? b : cmk(0.0, 0.0);
     }
 #pragma unroll
     for (int u = 0; u < kCCH; ++u) {
@@ -602,12 +606,10 @@ __device__ __forceinline__ void coop_row_inv(const Geo& G, const Part& D, const 
     for (int j0 = 0; j0 < G.W; j0 += kBlock * kCCH) {
       V v0[kCCH], v1[kCCH];
 #pragma unroll
-      for (int u = 0; u < kCCH; ++u) {
-        const int j = j0 + t + kBlock * u;
-        if (j < G.W) {
-          v0[u] = ld(r, j);
-          if (two) v1[u] = ld(r + 1, j);
-        }
+      for (int u = 0; u < kCCH; ++u) {  // clamped, branch-free
+        const int j = min(j0 + t + kBlock * u, G.W - 1);
+        v0[u] = ld(r, j);
+        v1[u] = ld(two ? r + 1 : r, j);
       }
 #pragma unroll
       for (int u = 0; u < kCCH; ++u) {
@@ -666,9 +668,10 @@ __device__ __forceinline__ void coop_col_conv(const Geo& G, const Part& D, cd* s
     for (int p0 = 0; p0 < G.P; p0 += kBlock * kCCH) {
       cd cv[kCCH];
 #pragma unroll
-      for (int u = 0; u < kCCH; ++u) {
+      for (int u = 0; u < kCCH; ++u) {  // clamped, branch-free
         const int p = p0 + t + kBlock * u;
-        cv[u] = (p < G.H) ? col[p] : cmk(0.0, 0.0);
+        const cd c = col[min(p, G.H - 1)];
+        cv[u] = (p < G.H) ? c : cmk(0.0, 0.0);
       }
 #pragma unroll
       for (int u = 0; u < kCCH; ++u) {
@@ -681,10 +684,7 @@ __device__ __forceinline__ void coop_col_conv(const Geo& G, const Part& D, cd* s
     for (int p0 = 0; p0 < G.P; p0 += kBlock * kCCH) {
       cd tv[kCCH];
 #pragma unroll
-      for (int u = 0; u < kCCH; ++u) {
-        const int p = p0 + t + kBlock * u;
-        if (p < G.P) tv[u] = tk[p];
-      }
+      for (int u = 0; u < kCCH; ++u) tv[u] = tk[min(p0 + t + kBlock * u, G.P - 1)];
 #pragma unroll
       for (int u = 0; u < kCCH; ++u) {
         const int p = p0 + t + kBlock * u;
@@ -794,13 +794,12 @@ __device__ __forceinline__ void gather_pair(const Geo& G, const cd* spec, int ld
   for (int k0 = lane; k0 < G.Qh; k0 += 64 * kGCH) {
     cd A[kGCH], B[kGCH];
 #pragma unroll
-    for (int u = 0; u < kGCH; ++u) {
-      const int k = k0 + 64 * u;
-      if (k < G.Qh) {
-        const cd* col = spec + (size_t)k * ld + r;
-        A[u] = col[0];
-        B[u] = two ? col[1] : cmk(0.0, 0.0);
-      }
+    for (int u = 0; u < kGCH; ++u) {  // clamped, branch-free
+      const int k = min(k0 + 64 * u, G.Qh - 1);
+      const cd* col = spec + (size_t)k * ld + r;
+      A[u] = col[0];
+      const cd bk = col[two ? 1 : 0];
+      B[u] = two ? bk : cmk(0.0, 0.0);
     }
 #pragma unroll
     for (int u = 0; u < kGCH; ++u) {

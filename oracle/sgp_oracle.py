@@ -315,6 +315,7 @@ def _solve(gn, psf, bkg, *, variant, init_recon=0, proj_type=0, stop_criterion=0
     times = np.zeros(MAXIT + 1)
     E_p = 0
     E_ls = 0
+    ls_trials = []  # line-search trials of every iteration (stats['ls_trials'])
     pst = {}
     if proj_type == 0:  # :248-253
         x[x < 0] = 0
@@ -369,6 +370,7 @@ def _solve(gn, psf, bkg, *, variant, init_recon=0, proj_type=0, stop_criterion=0
         fcontinue = 1
         d_tf = A(d)
         fr = max(Fold)
+        E_ls0 = E_ls
         while fcontinue:
             E_ls += 1
             xplus = x + lam * d
@@ -388,6 +390,7 @@ def _solve(gn, psf, bkg, *, variant, init_recon=0, proj_type=0, stop_criterion=0
                 yk = gtemp - g
                 g = gtemp.copy()
                 fcontinue = 0
+                ls_trials.append(E_ls - E_ls0)
             else:
                 lam = lam * beta
                 if variant == "beta" and adapt_beta:  # :798-800
@@ -438,7 +441,7 @@ def _solve(gn, psf, bkg, *, variant, init_recon=0, proj_type=0, stop_criterion=0
             break
     x = x.reshape(_shape) * scaling
     if stats is not None:
-        stats.update(E_p=E_p, E_ls=E_ls, beta=betaParam)
+        stats.update(E_p=E_p, E_ls=E_ls, beta=betaParam, ls_trials=ls_trials)
     return x, iter_ - 1, discr[0:iter_], times[0:iter_], None
 
 
