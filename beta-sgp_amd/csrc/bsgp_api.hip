@@ -164,10 +164,11 @@ struct bsgp_plan_s {
 // strides row chunks of cp = nfw*W pairs over the members).
 static int proj_list_cap(const Geo& g, int T) {
   const long npair = ((long)g.H * g.W + 1) / 2;
-  if (T == 1) return (int)(2 * ((npair + kBlock - 1) / kBlock));
+  const int nb = plan_block(g);
+  if (T == 1) return (int)(2 * ((npair + nb - 1) / nb));
   const long cp = (long)g.nfw * g.W;
   const long nch = (npair + cp - 1) / cp;
-  return (int)(2 * ((nch + T - 1) / T) * ((cp + kBlock - 1) / kBlock));
+  return (int)(2 * ((nch + T - 1) / T) * ((cp + nb - 1) / nb));
 }
 
 static int ensure_plist(bsgp_plan p, size_t n) {
@@ -332,7 +333,7 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   // one FFT buffer also stages a row pair's stored spectrum (2*Qh, row_inv2); odd spreads banks
   g.lpad = (maxlen + 1 > 2 * g.Qh ? maxlen + 1 : 2 * g.Qh) | 1;
   // LDS: nfw waves x 2 buffers, + reduction scratch
-  const size_t red_bytes = (size_t)kWaves * kMaxRed * sizeof(double) + kSharedBytes;
+  size_t red_bytes = (size_t)kWaves * kMaxRed * sizeof(double) + kSharedBytes;
   int nfw = kWaves;
   size_t budget = 160 * 1024 / 4 - 256;  // four workgroups per CU
   p->wg_per_cu = 4;
@@ -344,6 +345,8 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
     g.coop = 1;
     nfw = 1;
     budget = 160 * 1024 - 256;
+    // wave partials of the cooperative build's workgroups (kCoopBlock threads)
+    red_bytes = (size_t)(kCoopBlock / 64) * kMaxRed * sizeof(double) + kSharedBytes;
     if (need(1) > budget) {
       delete p;
       return fail(BSGP_ERR_UNSUPPORTED, "FFT length too large for one workgroup's LDS");
@@ -371,6 +374,11 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         ncu > 0)
       p->ncu = ncu;
+  }
+  if (BSGP_COOP512 && (bsgp_c512_args_size() != sizeof(SolveArgs) ||
+                       bsgp_c512_block() != kCoopBlock)) {
+    delete p;
+    return fail(BSGP_ERR_HIP, "cooperative 512-thread build does not match this library");
   }
   if (set_solver_lds_limit(p->lds_bytes) != hipSuccess) {
     delete p;
@@ -698,7 +706,7 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
                  : 4096;
   if (prm->proj_cache && prm->proj_type == 1) {
     a.lcap = proj_list_cap(p->g, T);
-    const size_t half = round_up((size_t)a.lcap * T * kBlock, 32);
+    const size_t half = round_up((size_t)a.lcap * T * plan_block(p->g), 32);
     a.plist_stride = 2 * half;
     rc = ensure_plist(p, (size_t)B * a.plist_stride);
     if (rc) return rc;

@@ -118,4 +118,27 @@ hipError_t launch_psf_stamps(const PsfModel& m, const double* xy, int n, int spa
                              int normalize, double* out, hipStream_t s);
 hipError_t phase_prof(unsigned long long* out, int n, int reset);
 
+// Cooperative plans (Geo::coop) run the phase kernels of bsgp_solver_c512.hip:
+// the same kernels with 512-thread workgroups (two waves per SIMD per
+// workgroup where a long transform's LDS allows one or two workgroups per CU).
+#ifndef BSGP_COOP512
+#define BSGP_COOP512 1
+#endif
+constexpr int kCoopBlock = BSGP_COOP512 ? 512 : kBlock;
+// threads per workgroup of a plan's phase kernels
+__host__ __device__ inline int plan_block(const Geo& g) { return g.coop ? kCoopBlock : kBlock; }
+
 }  // namespace bsgp
+
+// bsgp_solver_c512.hip (C linkage: its types live in namespace bsgp_c512; the
+// argument block is this header's SolveArgs, same layout)
+extern "C" {
+size_t bsgp_c512_args_size(void);
+int bsgp_c512_block(void);
+int bsgp_c512_waves(void);
+hipError_t bsgp_c512_launch_setup(const void* a, size_t lds, hipStream_t s);
+hipError_t bsgp_c512_launch_iteration(const void* a, int K, size_t lds, hipStream_t s,
+                                      hipEvent_t* ev);
+hipError_t bsgp_c512_team_resident(int storage, size_t lds, int* per_cu);
+hipError_t bsgp_c512_set_lds_limit(size_t bytes);
+}

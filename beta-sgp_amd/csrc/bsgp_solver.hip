@@ -256,15 +256,18 @@ __global__ void grad_parts_kernel(int64_t n, const double* den, const double* gn
 // keep each build's register allocation its own.
 // ----------------------------------------------------------- launchers
 hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s) {
+  if (a.g.coop && BSGP_COOP512) return bsgp_c512_launch_setup(&a, lds, s);
   if (a.storage == BSGP_STORAGE_F32) return launch_setup_f32(a, lds, s);
   return a.g.coop ? launch_setup_t<true, double>(a, lds, s) : launch_setup_t<false, double>(a, lds, s);
 }
 hipError_t launch_iteration(const SolveArgs& a, int K, size_t lds, hipStream_t s, hipEvent_t* ev) {
+  if (a.g.coop && BSGP_COOP512) return bsgp_c512_launch_iteration(&a, K, lds, s, ev);
   if (a.storage == BSGP_STORAGE_F32) return launch_iteration_f32(a, K, lds, s, ev);
   return a.g.coop ? launch_iteration_t<true, double>(a, K, lds, s, ev)
                   : launch_iteration_t<false, double>(a, K, lds, s, ev);
 }
 hipError_t team_resident_per_cu(bool coop, int storage, size_t lds, int* per_cu) {
+  if (coop && BSGP_COOP512) return bsgp_c512_team_resident(storage, lds, per_cu);
   std::vector<const void*> fns;
   if (storage == BSGP_STORAGE_F32)
     solver_kernels_f32(fns, coop);
@@ -387,7 +390,7 @@ hipError_t set_solver_lds_limit(size_t bytes) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return e;
   }
-  return hipSuccess;
+  return BSGP_COOP512 ? bsgp_c512_set_lds_limit(bytes) : hipSuccess;
 }
 
 }  // namespace bsgp
