@@ -141,4 +141,5 @@ hipError_t bsgp_c512_launch_iteration(const void* a, int K, size_t lds, hipStrea
                                       hipEvent_t* ev);
 hipError_t bsgp_c512_team_resident(int storage, size_t lds, int* per_cu);
 hipError_t bsgp_c512_set_lds_limit(size_t bytes);
+hipError_t bsgp_c512_phase_prof(unsigned long long* out, int n, int reset);
 }

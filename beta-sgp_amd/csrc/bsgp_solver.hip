@@ -23,6 +23,13 @@ hipError_t phase_prof(unsigned long long* out, int n, int reset) {
     unsigned long long z[kPhaseSlots] = {};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z);
   }
+  // the cooperative 512-thread build keeps its own counters: add them
+  if (e == hipSuccess && BSGP_COOP512) {
+    unsigned long long c[kPhaseSlots] = {};
+    e = bsgp_c512_phase_prof(c, n, reset);
+    if (e == hipSuccess && out)
+      for (int i = 0; i < n; ++i) out[i] += c[i];
+  }
   return e;
 #else
   (void)out;

@@ -63,6 +63,24 @@ hipError_t bsgp_c512_team_resident(int storage, size_t lds, int* per_cu) {
   return bsgp_c512::team_resident(fns, lds, per_cu);
 }
 
+// phase-profile counters of this build (-DBSGP_PHASE_PROF; bsgp_solver.hip adds them)
+hipError_t bsgp_c512_phase_prof(unsigned long long* out, int n, int reset) {
+#ifdef BSGP_PHASE_PROF
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(bsgp_c512::g_phase),
+                                     n * sizeof(unsigned long long));
+  if (e == hipSuccess && reset) {
+    unsigned long long z[bsgp_c512::kPhaseSlots] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(bsgp_c512::g_phase), z, sizeof z);
+  }
+  return e;
+#else
+  (void)out;
+  (void)n;
+  (void)reset;
+  return hipSuccess;
+#endif
+}
+
 hipError_t bsgp_c512_set_lds_limit(size_t bytes) {
   std::vector<const void*> fns = {(const void*)bsgp_c512::k_col<true>};
   bsgp_c512::kernels_of(fns, BSGP_STORAGE_F64);
