@@ -7,6 +7,8 @@
 // (sgp_betaDiv), restoration/flux_conserve_proj.py:7-144 (projectDF).
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
 #include <type_traits>
 #include <vector>
 
@@ -380,7 +382,18 @@ hipError_t launch_grad_parts(int64_t n, const double* den, const double* gn, dou
                      beta, pow1, w);
   return hipGetLastError();
 }
+// The dynamic-LDS limit is a per-function attribute shared by every plan: it
+// only ever rises (per device), so creating a plan with a short transform
+// after one with a long transform cannot lower the limit the first one's
+// launches need.
 hipError_t set_solver_lds_limit(size_t bytes) {
+  static std::mutex mu;
+  static std::map<int, size_t> applied;
+  int dev = 0;
+  hipError_t ge = hipGetDevice(&dev);
+  if (ge != hipSuccess) return ge;
+  std::lock_guard<std::mutex> lock(mu);
+  if (applied[dev] >= bytes) return hipSuccess;
   std::vector<const void*> fns = {
       (const void*)k_col<false>, (const void*)k_col<true>,
       (const void*)apply_op_kernel<false>, (const void*)apply_op_kernel<true>,
@@ -397,7 +410,9 @@ hipError_t set_solver_lds_limit(size_t bytes) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return e;
   }
-  return BSGP_COOP512 ? bsgp_c512_set_lds_limit(bytes) : hipSuccess;
+  hipError_t e = BSGP_COOP512 ? bsgp_c512_set_lds_limit(bytes) : hipSuccess;
+  if (e == hipSuccess) applied[dev] = bytes;
+  return e;
 }
 
 }  // namespace bsgp

@@ -96,6 +96,24 @@ def test_operator_2048_matches_numpy(B):
         assert rel(out, ref) < 1e-13
 
 
+def test_small_plan_after_large_keeps_lds_limit(B):
+    """The kernels' dynamic-LDS limit is shared by every plan and only rises:
+    a 64x64 plan created after a 2048x2048 one (cooperative transforms, > 64 KiB
+    of LDS) must leave the large plan's launches valid."""
+    rng = np.random.default_rng(5)
+    psf = np.zeros((2048, 2048))
+    psf[1024 - 8:1024 + 8, 1024 - 8:1024 + 8] = rng.uniform(0, 1, (16, 16))
+    psf /= psf.sum()
+    big = B.Plan(2048, 2048, psf, B.BSGP_CONV_CIRCULAR)
+    small = B.Plan(64, 64, np.full((5, 5), 1 / 25.0), B.BSGP_CONV_LINEAR_FILL)
+    x = rng.uniform(0, 1, (2048, 2048))
+    out = big.apply(B.to_dev(x[None])).cpu().numpy()[0]
+    ref = np.fft.irfft2(np.fft.rfft2(np.fft.fftshift(psf)) * np.fft.rfft2(x), s=x.shape)
+    assert rel(out, ref) < 1e-13
+    xs = rng.uniform(0, 1, (64, 64))
+    assert np.isfinite(small.apply(B.to_dev(xs[None])).cpu().numpy()).all()
+
+
 def test_odd_circular_operator_fftshift_quirk(B):
     """31x31: fftshift puts the PSF centre at n-1."""
     psf = np.zeros((31, 31))
