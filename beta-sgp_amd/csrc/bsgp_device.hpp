@@ -308,16 +308,54 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
       (long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
+// A member's block totals of NV sums and NM maxima, stored straight to its
+// partial slot `dst` (T > 1): wave partials to LDS, one barrier, then lane i <
+// NV + NM of wave 0 folds value i over the waves in block_sum's / block_max's
+// order (the same bits) and stores it.  The totals are not broadcast inside
+// the member (only the team totals are), which saves block_sum's and
+// block_max's other barriers; the stores are wave 0's, so the reduction
+// barrier's drain in thread 0 covers them.
+template <int NV, int NM>
+__device__ __forceinline__ void member_partials(const double* v, const double* mx, double* red,
+                                                double* dst) {
+  static_assert(NV + NM <= kMaxRed && NV + NM <= 64, "too many values");
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const double s = wave_sum(v[i]);
+    if (lane == 0) red[w * kMaxRed + i] = s;
+  }
+#pragma unroll
+  for (int k = 0; k < NM; ++k) {
+    const double s = wave_max(mx[k]);
+    if (lane == 0) red[w * kMaxRed + NV + k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < NV + NM) {
+    const int i = threadIdx.x;
+    double s = red[i];
+    if (i < NV) {
+      for (int k = 1; k < kWaves; ++k) s += red[k * kMaxRed + i];
+    } else {
+      for (int k = 1; k < kWaves; ++k) {
+        const double u = red[k * kMaxRed + i];
+        s = (u > s || u != u) ? u : s;
+      }
+    }
+    st_sc1(dst + i, s);
+  }
+}
+
 // Team sum of NV values: every thread of every member gets the totals.
 template <int NV>
 __device__ __forceinline__ void team_sum(double (&v)[NV], double* red, Team& t) {
-  block_sum<NV>(v, red);
-  if (t.T == 1) return;
-  double* slot = t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) st_sc1(slot + (size_t)t.m * kMaxRed + i, v[i]);
+  if (t.T == 1) {
+    block_sum<NV>(v, red);
+    return;
   }
+  double* slot = t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
+  const double none[1] = {0.0};
+  member_partials<NV, 0>(v, none, red, slot + (size_t)t.m * kMaxRed);
   team_red_barrier(t);
   // wave 0: lane l loads the partials of members l, l+64, ... (all loads in
   // flight at once), then a fixed shuffle tree: same order in every member
@@ -352,17 +390,14 @@ template <int NV, int NM>
 __device__ __forceinline__ void team_reduce(double (&v)[NV > 0 ? NV : 1], double (&mx)[NM], double* red,
                                             Team& t) {
   static_assert(NV + NM <= kMaxRed, "too many values");
+  if (t.T == 1) {
 #pragma unroll
-  for (int k = 0; k < NM; ++k) mx[k] = block_max(mx[k], red);
-  if constexpr (NV > 0) block_sum<NV>(v, red);
-  if (t.T == 1) return;
-  double* slot = t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) st_sc1(slot + (size_t)t.m * kMaxRed + i, v[i]);
-#pragma unroll
-    for (int k = 0; k < NM; ++k) st_sc1(slot + (size_t)t.m * kMaxRed + NV + k, mx[k]);
+    for (int k = 0; k < NM; ++k) mx[k] = block_max(mx[k], red);
+    if constexpr (NV > 0) block_sum<NV>(v, red);
+    return;
   }
+  double* slot = t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
+  member_partials<NV, NM>(v, mx, red, slot + (size_t)t.m * kMaxRed);
   team_red_barrier(t);
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
