@@ -390,10 +390,10 @@ template <int NV, int NM>
 __device__ __forceinline__ void team_reduce(double (&v)[NV > 0 ? NV : 1], double (&mx)[NM], double* red,
                                             Team& t) {
   static_assert(NV + NM <= kMaxRed, "too many values");
-  if (t.T == 1) {
+  if (t.T == 1) {  // sums first, then maxima: the order of team_sum + team_max
+    if constexpr (NV > 0) block_sum<NV>(v, red);
 #pragma unroll
     for (int k = 0; k < NM; ++k) mx[k] = block_max(mx[k], red);
-    if constexpr (NV > 0) block_sum<NV>(v, red);
     return;
   }
   double* slot = t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;

@@ -1019,9 +1019,13 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
         umax = (au > umax || au != au || !(a > 0)) ? (a > 0 ? au : INFINITY) : umax;
       }
     });
-    // (team_sum_max here, one team barrier less, measured 2 % slower on C4)
-    team_sum<N1>(t1, red, tm);
-    if (series) rho = team_max(umax, red, tm);
+    // sums and max|u| in one team barrier (the same bits as team_sum + team_max)
+    if (series) {
+      team_sum_max<N1>(t1, umax, red, tm);
+      rho = umax;
+    } else {
+      team_sum<N1>(t1, red, tm);
+    }
     PH_ADD(4, tk0);
     if (series && threadIdx.x == 0) {
       for (int m = 0; m <= MS; ++m) {
