@@ -37,11 +37,6 @@ import subprocess
 import sys
 import time
 
-# 8 hardware queues for this process (read by the HIP runtime when torch
-# initialises it): the solve then runs 8 sub-batches instead of 4 (+2.8 % on
-# C3).  Set before torch is imported; inherited by spawned ranks.
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("BSGP_BENCH_HW_QUEUES", "8")
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for p in (ROOT, os.path.join(ROOT, "beta-sgp_amd"), os.path.join(ROOT, "oracle")):
     if p not in sys.path:
@@ -117,15 +112,16 @@ def synth_batch(B, n, k, nstars, seed0, bkg=100.0, circular=False):
 
 
 def solve_kwargs(maxit, ls_spec, streams=None, team=None, circular=False, proj_cache=None,
-                 storage="f64"):
+                 storage="f64", persistent=None, stop3=False):
     max_projs, gamma, beta, alpha_min, alpha_max, alpha, M_alpha, tau, M = (
         1000, 1e-4, 0.4, 1e-5, 1e5, 1e1, 3, 0.5, 1)  # sgp.DEFAULT_PARAMS (sgp.py:34)
-    return dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=maxit, gamma=gamma, beta=beta,
+    return dict(init_recon=2, proj_type=1, stop_criterion=3 if stop3 else 1, MAXIT=maxit,
+                tol_convergence=1e-5, gamma=gamma, beta=beta,
                 alpha=alpha, alpha_min=alpha_min, alpha_max=alpha_max, M_alpha=M_alpha, tau=tau,
                 M=M, max_projs=max_projs, ccd_sat_level=65000.0, scale_data=True,
                 use_original_SGP_Afunction=circular, adapt_beta=False, betaParam=1.05, lr=1e-3,
                 lr_exp_param=0.1, schedule_lr=True, ls_spec=ls_spec, streams=streams,
-                team=team, proj_cache=proj_cache, storage=storage)
+                team=team, proj_cache=proj_cache, storage=storage, persistent=persistent)
 
 
 def cpu_model():
@@ -144,7 +140,7 @@ def cpu_baseline(n, k, nstars, images, maxit, workers, circular=False):
     wall time of the solve phase (pool already warm, inputs built in-task)."""
     import cpu_bench
     kw = solve_kwargs(maxit, None, circular=circular)
-    for key in ("ls_spec", "team", "streams", "proj_cache", "storage"):
+    for key in ("ls_spec", "team", "streams", "proj_cache", "storage", "persistent"):
         kw.pop(key)
     iters, wall, cpu_s = cpu_bench.run_pool(n, k, nstars, images, kw, workers)
     ncpu = os.cpu_count() or 1
@@ -263,6 +259,11 @@ def parse_args(argv=None):
                     help="workgroups per image (0/None = auto, 1 = one per image)")
     ap.add_argument("--proj-cache", type=int, default=None)
     ap.add_argument("--storage", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--persistent", type=int, default=None,
+                    help="1: every iteration in one persistent launch (task queue), 0: phase "
+                         "kernels per iteration (default: sgp.PERSIST_DEFAULT)")
+    ap.add_argument("--stop3", action="store_true",
+                    help="stop rule 3 (tol 1e-5, the application's) instead of stop rule 1")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true",
                     help="skip the profiled solve (per-kernel roofline)")
@@ -276,6 +277,12 @@ def parse_args(argv=None):
 
 
 def main():
+    # 8 hardware queues for this process (read by the HIP runtime when torch
+    # initialises it): the solve then runs 8 sub-batches instead of 4 (+2.8 % on
+    # C3).  Set here, before torch is imported, and inherited by
+    # spawned ranks; importing bench (tests/bench_path.py) leaves the
+    # environment alone.
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("BSGP_BENCH_HW_QUEUES", "8")
     args = parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -302,7 +309,8 @@ def main():
         B = args.batch if args.batch else cfg["batch"]
         seed0 = shard_seed0(rank, B)
     kw = solve_kwargs(args.maxit, args.ls_spec, args.streams, args.team, circular=circ,
-                      proj_cache=args.proj_cache, storage=args.storage)
+                      proj_cache=args.proj_cache, storage=args.storage,
+                      persistent=args.persistent, stop3=args.stop3)
 
     if args.stub:
         def step():
@@ -395,7 +403,10 @@ def main():
                              "team": int(cnt[0, 5]),
                              "proj_cache": kw["proj_cache"] if kw["proj_cache"] is not None
                              else sgp.PROJ_CACHE_DEFAULT,
-                             "gn_compact": sgp.GN_COMPACT_DEFAULT, "storage": args.storage})
+                             "gn_compact": sgp.GN_COMPACT_DEFAULT, "storage": args.storage,
+                             "persistent": kw["persistent"] if kw["persistent"] is not None
+                             else sgp.PERSIST_DEFAULT,
+                             "stop_criterion": kw["stop_criterion"]})
     if not args.no_profile:
         result["roofline"] = roofline(args, kw, gn, psf, bkg, B, n, kern_ms)
     if world == 1 and not args.no_cpu:
@@ -407,8 +418,11 @@ def main():
     print(json.dumps(result), flush=True)
 
 
-def roofline(args, kw, gn, psf, bkg, B, n, solve_ms):
-    """Per-kernel roofline from one profiled solve (outside the timed loop)."""
+def profile_kernels(kw, gn, psf, bkg, n):
+    """One profiled solve (bsgp_solve_profiled: one stream, a HIP event pair
+    around every kernel launch): per kernel class its span, launches and
+    algorithmic bytes per launch.  The persistent solver (k_persist) is one
+    launch that runs every phase of every iteration: its bytes are all of them."""
     import _bsgp
     import sgp
     prof = sgp.sgp_betaDiv_batch(gn, psf, bkg, profile=True, **kw)
@@ -419,7 +433,8 @@ def roofline(args, kw, gn, psf, bkg, B, n, solve_ms):
     kb = kernel_bytes(n, n, plan.P, plan.Q // 2 + 1, cnt, iters, beta=True, series=True,
                       compact=sgp.GN_COMPACT_DEFAULT == 1, bmap=False,
                       fused_at_col=(team == 1), vb=4.0 if kw["storage"] == "f32" else 8.0)
-    names = ["k_setup", "k_dir", "k_col", "k_ls", "k_bb"]
+    kb["k_persist"] = float(sum(kb.values()))
+    names = ["k_setup", "k_dir", "k_col", "k_ls", "k_bb", "k_persist"]
     ms, nl = prof["kernel_ms"], prof["launches"]
     kernels = {}
     for i, name in enumerate(names):
@@ -432,33 +447,47 @@ def roofline(args, kw, gn, psf, bkg, B, n, solve_ms):
         kernels[name] = {"ms_total": float(ms[i]), "launches": int(nl[i]),
                          "ms_per_launch": float(per_ms), "bytes_per_launch": float(per_b),
                          "achieved": float(ach), "frac": float(ach / HBM_PEAK_GBS)}
-    dom = max(names[1:], key=lambda k_: kernels[k_]["ms_total"])
+    alg_total = float(sum(v for k, v in kb.items() if k != "k_persist"))
+    return kernels, alg_total, cnt, iters, float(np.sum(ms))
+
+
+def roofline(args, kw, gn, psf, bkg, B, n, solve_ms):
+    """Per-kernel roofline from a profiled solve (outside the timed loop)."""
+    kernels, alg_total, cnt, iters, prof_total = profile_kernels(kw, gn, psf, bkg, n)
+    names = [k for k in kernels if k != "k_setup" and kernels[k]["launches"] > 0]
+    dom = max(names, key=lambda k_: kernels[k_]["ms_total"])
     d = kernels[dom]
-    prof_total = float(np.sum(ms))
-    alg_total = float(sum(kb.values()))
     traffic = load_traffic(args.config)
     tr = None
     if traffic and isinstance(traffic.get("kernels"), dict) and dom in traffic["kernels"]:
         tr = traffic["kernels"][dom].get("bytes_per_launch")
-    return {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": d["frac"], "traffic": tr,
-            "ms_per_launch": d["ms_per_launch"], "bytes_per_launch": d["bytes_per_launch"],
-            "launch_unit": f"one launch = {B} images x one iteration of {dom} "
-                           f"(profiled solve on one stream)",
-            "kernels": kernels,
-            "profiled_solve_ms": prof_total,
-            "solve": {"alg_bytes": alg_total, "ms_timed": solve_ms,
-                      "achieved_timed": alg_total / (solve_ms * 1e-3) / 1e9,
-                      "frac_timed": alg_total / (solve_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                      "note": "whole solve in the timed loop (sub-batch streams overlap "
-                              "kernels), same bytes"},
-            "counters_per_iter": {
-                "E_p": float(cnt[:, 0].sum() / iters.sum()),
-                "E_ls": float(cnt[:, 1].sum() / iters.sum()),
-                "proj_passes": float(cnt[:, 6].sum() / iters.sum()),
-                "proj_list_frac": float(cnt[:, 7].sum() / iters.sum() / (n * n)),
-                "ls_passes": float(cnt[:, 2].sum() / iters.sum()),
-                "ls_series": float(cnt[:, 4].sum() / iters.sum())}}
+    if dom == "k_persist":
+        unit = (f"one launch = the whole solve: {B} images x {int(iters.max())} iterations, "
+                f"every phase (persistent task-queue kernel)")
+    else:
+        unit = f"one launch = {B} images x one iteration of {dom} (profiled solve on one stream)"
+    out = {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": d["frac"], "traffic": tr,
+           "ms_per_launch": d["ms_per_launch"], "bytes_per_launch": d["bytes_per_launch"],
+           "launch_unit": unit, "kernels": kernels, "profiled_solve_ms": prof_total,
+           "solve": {"alg_bytes": alg_total, "ms_timed": solve_ms,
+                     "achieved_timed": alg_total / (solve_ms * 1e-3) / 1e9,
+                     "frac_timed": alg_total / (solve_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "note": "whole solve in the timed loop, same bytes"},
+           "counters_per_iter": {
+               "E_p": float(cnt[:, 0].sum() / iters.sum()),
+               "E_ls": float(cnt[:, 1].sum() / iters.sum()),
+               "proj_passes": float(cnt[:, 6].sum() / iters.sum()),
+               "proj_list_frac": float(cnt[:, 7].sum() / iters.sum() / (n * n)),
+               "ls_passes": float(cnt[:, 2].sum() / iters.sum()),
+               "ls_series": float(cnt[:, 4].sum() / iters.sum())}}
+    if dom == "k_persist":
+        # where the time goes, phase by phase: the same solve on the phase kernels
+        pk, _, _, _, ptot = profile_kernels(dict(kw, persistent=0), gn, psf, bkg, n)
+        out["phase_kernels"] = {"note": "the same solve as one launch per phase and iteration "
+                                        "(persistent=0), one stream", "profiled_solve_ms": ptot,
+                                "kernels": pk}
+    return out
 
 
 if __name__ == "__main__":

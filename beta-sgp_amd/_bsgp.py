@@ -27,7 +27,7 @@ BSGP_VARIANT_KL = 0
 BSGP_VARIANT_BETA = 1
 BSGP_STORAGE_F64 = 0
 BSGP_STORAGE_F32 = 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 BSGP_ERR_ARG = -1
 BSGP_ERR_HIP = -2
 BSGP_ERR_UNSUPPORTED = -3
@@ -59,7 +59,8 @@ class Params(ctypes.Structure):
         ("bkg_is_map", ctypes.c_int32), ("ls_spec", ctypes.c_int32), ("ls_series", ctypes.c_int32),
         ("streams", ctypes.c_int32), ("team", ctypes.c_int32), ("proj_cache", ctypes.c_int32),
         ("gn_compact", ctypes.c_int32), ("gn_f32", ctypes.c_int32),
-        ("beta0_general", ctypes.c_int32),
+        ("beta0_general", ctypes.c_int32), ("flux_f32", ctypes.c_int32),
+        ("persistent", ctypes.c_int32),
     ]
 
 
@@ -164,6 +165,9 @@ def current_stream():
 class Plan:
     """A device plan: FFT geometry + PSF transfer functions (bsgp_plan_create)."""
 
+    _leased = False  # held by a solve (lease_plan)
+    _done = None  # event after the last leased solve's launches
+
     def __init__(self, H, W, psf, conv_mode, device=None, storage=BSGP_STORAGE_F64):
         require_gpu()
         if device is None:
@@ -223,8 +227,8 @@ class Plan:
         "err" holds the per-iteration relative error); want_iterates adds
         "x_iter" [B,MAXIT,H,W].  Asynchronous on the current stream; returns a
         dict of device output tensors.  profile=True runs bsgp_solve_profiled
-        (one stream, synchronous) and adds "kernel_ms" / "launches" [5]: setup,
-        k_dir, k_col, k_ls, k_bb."""
+        (one stream, synchronous) and adds "kernel_ms" / "launches" [6]: setup,
+        k_dir, k_col, k_ls, k_bb, k_persist."""
         B = gn.shape[0]
         M1 = params.MAXIT + 1
         dev = gn.device
@@ -247,8 +251,8 @@ class Plan:
                                                  "beta_final", "counters", "err", "x_iter"]])
         self._keep = (gn, bkg, flux, x0, beta0, obj)
         if profile:
-            kms = np.zeros(5, np.float64)
-            nl = np.zeros(5, np.int64)
+            kms = np.zeros(6, np.float64)
+            nl = np.zeros(6, np.int64)
             check(lib().bsgp_solve_profiled(self.h, B, ctypes.byref(params), ctypes.byref(ins),
                                             ctypes.byref(outs), current_stream(),
                                             kms.ctypes.data, nl.ctypes.data))
@@ -294,30 +298,88 @@ def storage_code(storage):
     return STORAGE[storage]
 
 
-def get_plan(H, W, psf, conv_mode, storage="f64"):
-    """Plans are cached per (shape, psf bytes, mode, storage, device, host
-    thread): a plan's workspace belongs to one solve at a time (include/bsgp.h:
-    one plan per device per host thread), so threads never share one."""
-    require_gpu()
+def _plan_key(H, W, psf, conv_mode, storage):
     psf = np.ascontiguousarray(psf, dtype="<f8")
-    dev = torch.cuda.current_device()
-    st = storage_code(storage)
-    key = (H, W, psf.shape, psf.tobytes(), conv_mode, st, dev, threading.get_ident())
+    return psf, (H, W, psf.shape, psf.tobytes(), conv_mode, storage_code(storage),
+                 torch.cuda.current_device())
+
+
+def get_plan(H, W, psf, conv_mode, storage="f64"):
+    """A plan for the calling thread's own use (operators, plan queries):
+    cached per (shape, psf bytes, mode, storage, device, host thread), since a
+    plan's operator workspace serves one call at a time (include/bsgp.h: a
+    plan is not thread-safe).  Entries of threads that have ended are dropped.
+    Solves take their plan from the shared pool (lease_plan) instead."""
+    require_gpu()
+    psf, key = _plan_key(H, W, psf, conv_mode, storage)
+    key = key + (threading.get_ident(),)
     with _plan_cache_lock:
         p = _plan_cache.get(key)
         if p is None:
+            live = {t.ident for t in threading.enumerate()}
+            for k in [k for k in _plan_cache if k[-1] not in live]:
+                del _plan_cache[k]
             if len(_plan_cache) > 16:
                 _plan_cache.clear()
-            p = Plan(H, W, psf, conv_mode, dev, storage=st)
+            p = Plan(H, W, psf, conv_mode, key[6], storage=key[5])
             _plan_cache[key] = p
     return p
+
+
+# Solve plans: a pool per (shape, psf, mode, storage, device).  A solve leases
+# an idle plan (or creates one) for the duration of its enqueue; the plan's
+# workspace stays in use on the device until the solve's stream gets there, so
+# the lease ends with an event on that stream and the next lessee's stream
+# waits for it.  Concurrent solves (devices=[...] threads, several shards on
+# one GPU) get separate plans; later calls reuse them, whichever thread runs
+# them, so a new devices=[...] call re-allocates nothing.
+_pool = {}
+_POOL_MAX = 8  # plans kept per key
+
+
+class lease_plan:
+    """Context manager: ``with lease_plan(H, W, psf, mode, storage) as plan``."""
+
+    def __init__(self, H, W, psf, conv_mode, storage="f64"):
+        require_gpu()
+        self.args = (H, W, psf, conv_mode, storage)
+        self.plan = None
+
+    def __enter__(self):
+        H, W, psf, conv_mode, storage = self.args
+        psf, key = _plan_key(H, W, psf, conv_mode, storage)
+        with _plan_cache_lock:
+            plans = _pool.setdefault(key, [])
+            p = next((q for q in plans if not q._leased), None)
+            if p is None:
+                p = Plan(H, W, psf, conv_mode, key[6], storage=key[5])
+                p._done = None
+                if len(plans) < _POOL_MAX:
+                    plans.append(p)
+            p._leased = True
+        if p._done is not None:
+            torch.cuda.current_stream().wait_event(p._done)
+        self.plan = p
+        return p
+
+    def __exit__(self, *exc):
+        p = self.plan
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        p._done = ev
+        with _plan_cache_lock:
+            p._leased = False
+        return False
 
 
 def per_image_plan(H, W, psfs, conv_mode, storage="f64"):
     """A plan whose image i uses psfs[i] ([B, kh, kw], numpy or CUDA tensor);
     not cached (it holds B transfer-function pairs)."""
     require_gpu()
-    dev = psfs.to(dtype=torch.float64).contiguous() if torch.is_tensor(psfs) else to_dev(psfs)
+    # on the current device whatever device (or host) the stamps come from:
+    # the plan-building kernels read them there
+    dev = (psfs.to(device=torch.cuda.current_device(), dtype=torch.float64).contiguous()
+           if torch.is_tensor(psfs) else to_dev(psfs))
     p = Plan(H, W, dev[0].cpu().numpy(), conv_mode, storage=storage_code(storage))
     return p.set_psfs(dev)
 

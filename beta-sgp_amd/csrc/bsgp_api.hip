@@ -35,6 +35,28 @@ int fail(int code, const std::string& msg) {
 
 size_t round_up(size_t v, size_t m) { return (v + m - 1) / m * m; }
 
+// Every entry point that works on a plan's device makes it current for the
+// call and gives the caller's thread its own current device back on return
+// (a plan destroyed from a garbage-collector thread, or a solve on another
+// GPU, must not switch the device the caller's framework is using).
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    err = hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+#define DEVICE_SCOPE(dev)                                                                   \
+  DeviceGuard dev_guard_(dev);                                                              \
+  if (dev_guard_.err != hipSuccess)                                                         \
+    return fail(BSGP_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(dev_guard_.err))
+
 // numpy's float32 np.sum over n contiguous elements (numpy 1.26 and 2.x,
 // checked against np.sum in tests/test_oracle.py::test_numpy_f32_sum_model):
 // the reduction runs over chunks of 8192 (the ufunc buffer), folding
@@ -157,6 +179,9 @@ struct bsgp_plan_s {
   // numpy's float32 reduction order over N elements (gn_f32 solves)
   int* pwprog = nullptr;
   PwProg pw{};
+  // persistent solver: dequeue counter + per-image published iterations
+  unsigned* pq = nullptr;
+  size_t pq_n = 0;
 };
 
 // Capacity of one thread's projection list: the pixels it streams in one pass
@@ -242,7 +267,7 @@ static int ensure_team(bsgp_plan p, size_t B, int T) {
 
 extern "C" {
 
-int32_t bsgp_abi_version(void) { return 2; }
+int32_t bsgp_abi_version(void) { return 3; }
 
 // Diagnostics (not in include/bsgp.h): per-phase shader cycles of a build
 // with -DBSGP_PHASE_PROF; returns BSGP_ERR_UNSUPPORTED otherwise.
@@ -300,7 +325,7 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
       return fail(BSGP_ERR_PSF, b);
     }
   }
-  HIP_TRY(hipSetDevice(device));
+  DEVICE_SCOPE(device);
   bsgp_plan p = new bsgp_plan_s();
   p->device = device;
   p->conv_mode = conv_mode;
@@ -496,7 +521,7 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
 
 int bsgp_plan_destroy(bsgp_plan p) {
   if (!p) return BSGP_OK;
-  (void)hipSetDevice(p->device);
+  DeviceGuard dev_guard_(p->device);
   if (p->tw) (void)hipFree(p->tw);
   if (p->tf) (void)hipFree(p->tf);
   if (p->ws) (void)hipFree(p->ws);
@@ -513,6 +538,7 @@ int bsgp_plan_destroy(bsgp_plan p) {
   if (p->tctr) (void)hipFree(p->tctr);
   if (p->plist) (void)hipFree(p->plist);
   if (p->pwprog) (void)hipFree(p->pwprog);
+  if (p->pq) (void)hipFree(p->pq);
   delete p;
   return BSGP_OK;
 }
@@ -524,7 +550,7 @@ int bsgp_plan_set_psfs(bsgp_plan p, const double* psfs, int32_t n, void* stream)
   // the device placement stores (no accumulation): the kernel must not wrap on the grid
   if (!circ && (p->kh > g.P || p->kw > g.Q || p->kw > g.P || p->kh > g.Q))
     return fail(BSGP_ERR_ARG, "per-image PSFs need a kernel no larger than the FFT grid");
-  HIP_TRY(hipSetDevice(p->device));
+  DEVICE_SCOPE(p->device);
   hipStream_t s = (hipStream_t)stream;
   const size_t PQ = (size_t)g.P * g.Q, tfn = (size_t)g.Qh * g.P, specn = (size_t)g.P * g.Qh;
   // chunks bound the placement/spectrum workspace (~256 MiB)
@@ -604,8 +630,8 @@ static int check_params(const bsgp_params* q) {
   if (q->init_recon < 0 || q->init_recon > 3) return fail(BSGP_ERR_ARG, "bad init_recon");
   if (q->proj_type != 0 && q->proj_type != 1) return fail(BSGP_ERR_ARG, "bad proj_type");
   if (q->scale_data < 0 || q->scale_data > 2) return fail(BSGP_ERR_ARG, "bad scale_data");
-  if (q->gn_f32 && q->scale_data != 2)
-    return fail(BSGP_ERR_ARG, "gn_f32 needs scale_data == 2 (the caller scales in float32)");
+  if (q->flux_f32 && !(q->gn_f32 && q->scale_data != 2))
+    return fail(BSGP_ERR_ARG, "flux_f32 needs gn_f32 with scale_data 0 or 1");
   return BSGP_OK;
 }
 
@@ -630,7 +656,7 @@ int bsgp_solve_profiled(bsgp_plan p, int32_t B, const bsgp_params* prm, const bs
   if (!kernel_ms || !launches) return fail(BSGP_ERR_ARG, "kernel_ms / launches missing");
   if (!prm) return fail(BSGP_ERR_ARG, "params is NULL");
   if (!p) return fail(BSGP_ERR_ARG, "plan is NULL");
-  HIP_TRY(hipSetDevice(p->device));
+  DEVICE_SCOPE(p->device);
   SolveProf prof;
   prof.kernel_ms = kernel_ms;
   prof.launches = launches;
@@ -662,7 +688,7 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   if (out->err && !in->obj) return fail(BSGP_ERR_ARG, "err needs the ground truth obj");
   if (p->n_tf > 1 && B != p->n_tf)
     return fail(BSGP_ERR_ARG, "the plan holds one PSF per image: B must equal its PSF count");
-  HIP_TRY(hipSetDevice(p->device));
+  DEVICE_SCOPE(p->device);
   rc = ensure_ws(p, (size_t)B);
   if (rc) return rc;
   const int T = choose_team(p, B, prm->team);
@@ -722,6 +748,14 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   int S = prm->streams < 1 ? 1 : prm->streams;
   if (S > bsgp_plan_s::kMaxStreams) S = bsgp_plan_s::kMaxStreams;
   if (S > B) S = B;
+  // per-iteration error / iterate snapshots (errflag, save): one small kernel
+  // after setup and after every iteration, off the hot kernels
+  const bool track = out->err != nullptr || out->x_iter != nullptr;
+  // persistent solver (one launch for every iteration, k_persist): one-workgroup
+  // images with per-wave transforms; it overlaps the phases of different images
+  // itself, so it runs the whole batch as one sub-batch
+  const bool persist = prm->persistent && T == 1 && !p->g.coop && !track;
+  if (persist) S = 1;
   // sub-batch 0 runs on the caller's stream itself, sub-batches 1..S-1 on the
   // plan's streams: S streams in all, so S = 4 fits the 4 hardware queues HIP
   // opens per process (GPU_MAX_HW_QUEUES)
@@ -740,9 +774,6 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   HIP_TRY(hipMemsetAsync(p->tctr, 0, p->tctr_bytes, s));
   hipStream_t ss[bsgp_plan_s::kMaxStreams];
   SolveArgs sa[bsgp_plan_s::kMaxStreams];
-  // per-iteration error / iterate snapshots (errflag, save): one small kernel
-  // after setup and after every iteration, off the hot kernels
-  const bool track = out->err != nullptr || out->x_iter != nullptr;
   if (S > 1) HIP_TRY(hipEventRecord(p->ev_fork, s));
   for (int j = 0; j < S; ++j) {
     ss[j] = j > 0 ? p->sub[j] : s;
@@ -754,6 +785,41 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     HIP_TRY(launch_setup(sa[j], p->lds_bytes, ss[j]));
     if (prof) HIP_TRY(hipEventRecord(prof->ev[1], ss[j]));
     if (track) HIP_TRY(launch_track(sa[j], 0, ss[j]));
+  }
+  if (persist) {
+    const size_t need = (size_t)B + 1;  // queue word + done[B]
+    if (need > p->pq_n) {
+      if (p->pq) HIP_TRY(hipFree(p->pq));
+      p->pq = nullptr;
+      p->pq_n = 0;
+      HIP_TRY(hipMalloc(&p->pq, need * sizeof(unsigned)));
+      p->pq_n = need;
+    }
+    HIP_TRY(hipMemsetAsync(p->pq, 0, need * sizeof(unsigned), s));
+    int per_cu = 0;
+    HIP_TRY(persist_resident_per_cu(sa[0], K, p->lds_bytes, &per_cu));
+    if (per_cu < 1) return fail(BSGP_ERR_HIP, "persistent solver does not fit a CU");
+    // every workgroup resident at once (a dequeued task's predecessor is always
+    // running or done); no more workgroups than images
+    const int grid = (int)std::min<long>(B, (long)p->ncu * per_cu);
+    if (prof) HIP_TRY(hipEventRecord(prof->ev[2], s));
+    HIP_TRY(launch_persist(sa[0], K, p->lds_bytes, s, p->pq, p->pq + 1, grid));
+    if (prof) {
+      HIP_TRY(hipEventRecord(prof->ev[3], s));
+      HIP_TRY(hipStreamSynchronize(s));
+      for (int k = 0; k < 6; ++k) {
+        prof->kernel_ms[k] = 0.0;
+        prof->launches[k] = 0;
+      }
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, prof->ev[0], prof->ev[1]));
+      prof->kernel_ms[0] = ms;
+      prof->launches[0] = 1;
+      HIP_TRY(hipEventElapsedTime(&ms, prof->ev[2], prof->ev[3]));
+      prof->kernel_ms[5] = ms;
+      prof->launches[5] = 1;
+    }
+    return BSGP_OK;
   }
   // Fixed-length runs (stop_criterion 0/1) are launched back to back with no
   // host synchronisation; data-dependent stop rules poll the counter.
@@ -783,7 +849,7 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   if (prof) {
     // kernel classes: 0 setup, 1 dir, 2 col (A and AT launches), 3 ls, 4 bb
     HIP_TRY(hipStreamSynchronize(s));
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < 6; ++k) {
       prof->kernel_ms[k] = 0.0;
       prof->launches[k] = 0;
     }
@@ -812,7 +878,7 @@ int bsgp_solve_host(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp_i
   if (rc) return rc;
   if (B < 1 || !in || !in->gn || !in->bkg || !out || !out->x || !out->iters || !out->discr)
     return fail(BSGP_ERR_ARG, "bad arguments");
-  HIP_TRY(hipSetDevice(p->device));
+  DEVICE_SCOPE(p->device);
   const size_t N = (size_t)p->g.H * p->g.W, M1 = (size_t)prm->MAXIT + 1;
   std::vector<void*> bufs;
   auto dalloc = [&](size_t bytes) -> void* {
@@ -888,7 +954,7 @@ int bsgp_apply_operator(bsgp_plan p, int32_t B, int32_t transpose, const double*
   if (!p || !x || !out || B < 1) return fail(BSGP_ERR_ARG, "bad arguments");
   if (p->n_tf > 1 && B != p->n_tf)
     return fail(BSGP_ERR_ARG, "the plan holds one PSF per image: B must equal its PSF count");
-  HIP_TRY(hipSetDevice(p->device));
+  DEVICE_SCOPE(p->device);
   const int slots = p->ncu * p->wg_per_cu;
   // few images: spread each over many workgroups (rows, columns, rows), one
   // spectrum per image; many images: one persistent workgroup per image

@@ -4,6 +4,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "../../include/bsgp.h"
 #include "bsgp_device.hpp"
 
@@ -117,6 +119,13 @@ struct PsfModel;
 hipError_t launch_psf_stamps(const PsfModel& m, const double* xy, int n, int spatial,
                              int normalize, double* out, hipStream_t s);
 hipError_t phase_prof(unsigned long long* out, int n, int reset);
+// persistent task-queue solver (bsgp_persist.hip): one launch runs every
+// iteration of every image; queue = dequeue counter, done[B] = iterations
+// published per image (both zeroed per solve)
+hipError_t launch_persist(const SolveArgs& a, int K, size_t lds, hipStream_t s, unsigned* queue,
+                          unsigned* done, int grid);
+hipError_t persist_resident_per_cu(const SolveArgs& a, int K, size_t lds, int* per_cu);
+void persist_kernels_all(std::vector<const void*>& f);
 
 // Cooperative plans (Geo::coop) run the phase kernels of bsgp_solver_c512.hip:
 // the same kernels with 512-thread workgroups (two waves per SIMD per

@@ -397,23 +397,42 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   }
   team_sum_max<3>(v2, mx, red, tm);  // one team barrier
   const bool ok32 = v2[2] == 0.0;     // every raw value finite and exact in f32
+  // float32 image, prelude on the device (include/bsgp.h, ABI 3): numpy 1.x
+  // keeps gn / scaling and x / scaling in float32 (sgp.py:648-652)
+  const bool pre32 = P.gn_f32 && P.scale_data != 2;
   const double sc = P.scale_data == 2 ? P.prescaled_scaling : (P.scale_data ? mx : 1.0);
+  const float sc32 = (float)sc;  // exact: max of float32 values
   const double fl_raw = A.in.flux ? A.in.flux[img] : v2[0];
-  const double x3 = (fl_raw / (double)N) * 1.0;  // np.sum(gn-bkg)/gn.size*ones (sgp.py:175)
-  const double tol4 = P.scale_data == 2 ? P.prescaled_tol4 : 1 + 1 / (v2[1] / (double)N);
+  // np.sum(gn-bkg)/gn.size*ones (sgp.py:175); a float32 image keeps the float32 array
+  const double x3 = pre32 ? (double)(float)(fl_raw / (double)N) : (fl_raw / (double)N) * 1.0;
+  double tol4 = P.scale_data == 2 ? P.prescaled_tol4 : 1 + 1 / (v2[1] / (double)N);
+  if (pre32 && P.stop_criterion == 4) {
+    // 1 + 1/np.mean(gn) of the raw float32 image (sgp.py:644): numpy's float32
+    // pairwise sum, the mean rounded to float32, the rest in float64
+    const float s32 = np_f32_sum(
+        A.pw, [&](int i) { return (float)gn_in[i]; }, reinterpret_cast<float*>(B.dtf), D, tm);
+    tol4 = 1 + 1 / (double)(float)((double)s32 / (double)N);
+  }
   const bool divide = P.scale_data == 1;
-  const double bks_scalar = P.scale_data == 2 ? bk_scalar_raw : bk_scalar_raw / sc;
+  const double bks_scalar = P.scale_data == 2 ? bk_scalar_raw : (divide ? bk_scalar_raw / sc
+                                                                        : bk_scalar_raw);
+  // gn (and an init_recon 2 start) / scaling: float64, or float32 for a float32 image
+  auto scale_px = [&](double g) {
+    if (pre32) return divide ? (double)((float)g / sc32) : g;
+    return divide ? g / sc : g;
+  };
   // scale + null-pixel minimum (sgp.py:193-204)
   double vmin = INFINITY;
   for (int i = D.gt0 + tid; i < N; i += D.gts) {
-    const double g = divide ? gn_in[i] / sc : gn_in[i];
+    const double g = scale_px(gn_in[i]);
     B.gns[i] = g;
     if (g > 0 && g < vmin) vmin = g;
     if (bmap) B.bks[i] = divide ? bk_in[i] / sc : bk_in[i];
   }
   vmin = team_min(vmin, red, tm);
   const double eps = 2.220446049250313e-16;
-  const double fill = vmin * eps * eps;
+  // the fill is stored into the float32 array for a float32 image (sgp.py:659)
+  const double fill = pre32 ? (double)(float)(vmin * eps * eps) : vmin * eps * eps;
   double v1[1] = {0.0};
   for (int i = D.gt0 + tid; i < N; i += D.gts) {
     double g = B.gns[i];
@@ -425,15 +444,15 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     // initial x (sgp.py:166-177, 197), then the pflag==0 clamp (:248-249)
     double x;
     if (A.in.x0) {
-      x = A.in.x0[(size_t)img * N + i];
+      x = A.in.x0[(size_t)img * N + i];  // float64 (randn): x / scaling stays float64
+      if (divide) x = x / sc;
     } else if (P.init_recon == 0) {
       x = 0.0;
     } else if (P.init_recon == 2) {
-      x = gn_in[i];
+      x = scale_px(gn_in[i]);  // gn.copy() / scaling, before the null-pixel fix
     } else {
-      x = x3;
+      x = scale_px(x3);
     }
-    if (divide) x = x / sc;
     if (P.proj_type == 0 && x < 0) x = 0;
     B.xa[i] = x;
   }
@@ -444,8 +463,12 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   }
   team_sum<1>(v1, red, tm);
   // sgp.py:208-211 (scale_data 2: the caller scaled the flux in its own dtype)
+  // (a numpy float32 flux over the float32 scaling divides in float32)
   const double flux =
-      A.in.flux ? (P.scale_data == 2 ? A.in.flux[img] : A.in.flux[img] / sc) : v1[0];
+      A.in.flux ? (P.scale_data == 2 ? A.in.flux[img]
+                   : (pre32 && P.flux_f32 && divide) ? (double)((float)A.in.flux[img] / sc32)
+                                                     : A.in.flux[img] / sc)
+                : v1[0];
   const ProjClip clip{P.has_sat != 0, P.ccd_sat_level / sc - eps};
 
   // initial projection with dia = 1 (sgp.py:250-253); every thread clips the
@@ -535,10 +558,13 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   // half of its slot vector (every f64 read of gn_s is done: team_sync above).
   // Readers recompute gn_s = raw / sc (or raw), and the null-pixel fill for
   // raw <= 0, with the operations used above: the same bits as f64 storage.
-  const int g32 = (P.gn_compact && ok32) ? (divide ? (sc > 0 ? 2 : 0) : 1) : 0;
+  // A float32 image's scaled values are float32 themselves: kept as they are
+  // (mode 1), with the fill for values <= 0 on read.
+  const int g32 = (P.gn_compact && ok32) ? ((divide && !pre32) ? (sc > 0 ? 2 : 0) : 1) : 0;
   if (g32) {
     float* gf = reinterpret_cast<float*>(B.gns);
-    for (int i = D.gt0 + tid; i < N; i += D.gts) gf[i] = (float)gn_in[i];
+    for (int i = D.gt0 + tid; i < N; i += D.gts)
+      gf[i] = (float)(g32 == 2 ? gn_in[i] : scale_px(gn_in[i]));  // mode 2 divides on read
     if (odd && leader(tm)) gf[N] = 1.0f;  // pad element of the pair-vectorised streams
   }
   const double Dcoeff = 2 / (double)N * sc;
@@ -783,17 +809,16 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
 // sgp.py:306-325: memory shifts, y = x - alpha*X*g, projectDF(flux, y*D, D)
 // with every x(lambda) evaluation one streaming pass over (x, g), d = y - x,
 // d.g, and the row transforms of d.
+// One image's phase (the kernel below, or the persistent solver's task): the
+// caller has checked st.stop and loaded the twiddles into LDS.
 template <bool COOP, class V>
-__global__ void __launch_bounds__(kBlock) BSGP_DIR_ATTR k_dir(SolveArgs A) {
+__device__ __forceinline__ void dir_phase(const SolveArgs& A, int img) {
   BSGP_LDS_VIEWS(A);
-  const int img = team_img(A);
   ImgState& st = A.st[img];
-  if (st.stop) return;
   PH_T(tk0);
   Team tm = make_team(A, img, st);
   const Geo& G = A.g;
   const Part Pt = make_part(tm, G.nfw, G.W);
-  load_tw_lds(G);
   const bsgp_params& P = A.prm;
   const int N = G.H * G.W;
   const int npair = (N + 1) / 2;
@@ -877,6 +902,14 @@ __global__ void __launch_bounds__(kBlock) BSGP_DIR_ATTR k_dir(SolveArgs A) {
   }
 }
 
+template <bool COOP, class V>
+__global__ void __launch_bounds__(kBlock) BSGP_DIR_ATTR k_dir(SolveArgs A) {
+  const int img = team_img(A);
+  if (A.st[img].stop) return;
+  load_tw_lds(A.g);
+  dir_phase<COOP, V>(A, img);
+}
+
 // ----------------------------------------------------------- kernel: columns
 template <bool COOP>
 __global__ void __launch_bounds__(kBlock) BSGP_COL_ATTR k_col(SolveArgs A, int transpose) {
@@ -900,19 +933,16 @@ __global__ void __launch_bounds__(kBlock) BSGP_COL_ATTR k_col(SolveArgs A, int t
 // the first pass is fused into the inverse row transforms that produce d_tf.
 // Then x_tf += lam*d_tf and the row transforms of AT's input w.
 template <int K, int MODE, bool ADAPT, bool COOP, class V>
-__global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
+__device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
   // first pass (fused into the inverse rows of A(d)): one trial lambda = 1,
   // which is where most non-stagnating iterations accept; later passes
   // stream K trial lambdas each.
   BSGP_LDS_VIEWS(A);
-  const int img = team_img(A);
   ImgState& st = A.st[img];
-  if (st.stop) return;
   PH_T(tk0);
   Team tm = make_team(A, img, st);
   const Geo& G = A.g;
   const Part Pt = make_part(tm, G.nfw, G.W);
-  load_tw_lds(G);
   const bsgp_params& P = A.prm;
   const int N = G.H * G.W;
   const int npair = (N + 1) / 2;
@@ -1215,8 +1245,11 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   PH_ADD(7, tk0);
   team_end(st, tm);
   if (leader(tm)) {
+    // bit 0: the fv >= fr warning (sgp.py:803-804); bits 8..23: this
+    // iteration's line-search trials (the reference's betaDiv calls at :782)
     if (A.out.flags)
-      A.out.flags[(size_t)img * (P.MAXIT + 1) + st.iter] = (f_acc >= fr) ? 1 : 0;
+      A.out.flags[(size_t)img * (P.MAXIT + 1) + st.iter] =
+          ((f_acc >= fr) ? 1 : 0) | ((nls < 0xffff ? nls : 0xffff) << 8);
     st.fv = f_acc;
     st.beta = obj.beta;
     st.konst = konst;
@@ -1228,21 +1261,26 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   }
 }
 
+template <int K, int MODE, bool ADAPT, bool COOP, class V>
+__global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
+  const int img = team_img(A);
+  if (A.st[img].stop) return;
+  load_tw_lds(A.g);
+  ls_phase<K, MODE, ADAPT, COOP, V>(A, img);
+}
+
 // ------------------------------ kernel: gradient, x update, BB, stop rules
 // sgp.py:337-414 (= 785-879): g_new = g1(den) - AT(w), x += lam*d, the
 // Barzilai-Borwein step lengths with the tau alternation, the stop rules,
 // and the outputs once the image stops (sgp.py:424-438).
 template <bool COOP, class V>
-__global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
+__device__ __forceinline__ void bb_phase(const SolveArgs& A, int img) {
   BSGP_LDS_VIEWS(A);
-  const int img = team_img(A);
   ImgState& st = A.st[img];
-  if (st.stop) return;
   PH_T(tk0);
   Team tm = make_team(A, img, st);
   const Geo& G = A.g;
   const Part Pt = make_part(tm, G.nfw, G.W);
-  load_tw_lds(G);
   const bsgp_params& P = A.prm;
   const int N = G.H * G.W;
   const int tid = threadIdx.x;
@@ -1379,6 +1417,198 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
       atomicSub(A.active, 1);
     }
   }
+}
+
+template <bool COOP, class V>
+__global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
+  const int img = team_img(A);
+  if (A.st[img].stop) return;
+  load_tw_lds(A.g);
+  bb_phase<COOP, V>(A, img);
+}
+
+// ------------------------------------------- persistent task-queue solver
+// One-workgroup images with per-wave transforms (T == 1, the batched configs
+// C3/C5): ONE launch runs every iteration of every image of a sub-batch.  A
+// task is (iteration k, image i); tasks are dequeued in the order t = (k-1) *
+// nimg + (i - img0) from one device counter, so every resident workgroup has
+// work until the last iteration's tasks and no launch ends in a
+// partly-occupied round (1024 images on 768 slots are 1.33 rounds per
+// launch in the phase-kernel solve), and a CU holds workgroups in different
+// phases of their tasks at once (memory-bound row passes beside LDS-bound
+// transforms).  A task runs the phases of one iteration (dir_phase, A's
+// column pass, ls_phase with AT's column pass, bb_phase), the same device code
+// the phase kernels run, so the results are bit-identical to theirs.
+//
+// Iteration k of image i needs iteration k - 1 done, usually by another
+// workgroup on another CU or XCD.  Hand-off (MI355X_MICROARCH.md,
+// inter-workgroup visibility, valid producer/consumer forms): the producer's
+// waves drain their stores, a workgroup barrier, lane 0 releases at agent
+// scope and stores done[i] = k with a relaxed agent-scope (sc1) store; the
+// consumer's lane 0 polls done[i] with sc1 loads, acquires at agent scope,
+// and a workgroup barrier lets the other waves load.  The predecessor task
+// was dequeued earlier by a resident workgroup, so the wait always ends; the
+// poll is bounded anyway (timeout -> status bit 4, every workgroup leaves).
+// An image that stopped publishes kDoneStop | k: its later tasks are skipped
+// without a fence.  When no image is running the workgroups leave early.
+constexpr unsigned kDoneStop = 0x40000000u;
+
+#ifndef BSGP_PERSIST_ATTR
+#define BSGP_PERSIST_ATTR __attribute__((amdgpu_waves_per_eu(3)))
+#endif
+
+__device__ __forceinline__ unsigned ld_sc1_u32(const unsigned* p) {
+  return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The phases of a task are separate (noinline) functions, so each keeps the
+// register allocation of its own kernel; their argument block is re-read from
+// the kernarg segment (scalar loads) through a pointer the compiler cannot see
+// through.  Inlined into one kernel body the phases spilled 57-88 VGPRs inside
+// their loops at the 168 VGPRs of 3 waves/SIMD (the scalar state of all
+// phases at once); as calls the only spill code is each phase's callee-saved
+// registers at its entry and exit (~210 VGPRs per wave per task, ~3 % of a
+// task's bytes, L2-resident).
+#ifndef BSGP_PERSIST_CALLS
+#define BSGP_PERSIST_CALLS 1
+#endif
+__device__ __forceinline__ const SolveArgs& kernarg_args() {
+  typedef const __attribute__((address_space(4))) SolveArgs* KP;
+  KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const SolveArgs*)p;
+}
+#if BSGP_PERSIST_CALLS
+#define BSGP_PERSIST_FN __attribute__((noinline))
+#else
+#define BSGP_PERSIST_FN __forceinline__
+#endif
+template <class V>
+__device__ BSGP_PERSIST_FN void persist_dir(int img) {
+  dir_phase<false, V>(kernarg_args(), img);
+}
+__device__ BSGP_PERSIST_FN void persist_col_a(int img) {
+  const SolveArgs& A = kernarg_args();
+  BSGP_LDS_VIEWS(A);
+  (void)red;
+  Team tm{};
+  tm.T = 1;
+  const Bufs<double> Bd = slot_bufs<double>(A, img, 0);  // spec only (same offset for V)
+  PH_T(tc0);
+  col_conv<false>(A.g, make_part(tm, A.g.nfw, A.g.W), Bd.spec, tf_of(A.g, img, 0), lds);
+  PH_ADD(3, tc0);
+}
+template <int K, int MODE, bool ADAPT, class V>
+__device__ BSGP_PERSIST_FN void persist_ls(int img) {
+  ls_phase<K, MODE, ADAPT, false, V>(kernarg_args(), img);
+}
+template <class V>
+__device__ BSGP_PERSIST_FN void persist_bb(int img) {
+  bb_phase<false, V>(kernarg_args(), img);
+}
+
+template <int K, int MODE, bool ADAPT, class V>
+__global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs A,
+                                                                        unsigned* queue,
+                                                                        unsigned* done) {
+  BSGP_LDS_VIEWS(A);
+  (void)red;
+  __shared__ unsigned s_task, s_skip;
+  const int tid = threadIdx.x;
+  const Geo& G = A.g;
+  load_tw_lds(G);
+  const unsigned nimg = (unsigned)A.nimg;
+  const unsigned total = (unsigned)A.prm.MAXIT * nimg;
+  for (;;) {
+    if (tid == 0) {
+      unsigned t = atomicAdd(queue, 1u);
+      unsigned skip = 0;
+      if (t < total && __hip_atomic_load((gi32*)A.active, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) <= 0)
+        t = total;  // every image has stopped: nothing left to run
+      if (t < total) {
+        const int img = A.img0 + (int)(t % nimg);
+        const unsigned need = t / nimg;  // iterations of img that must be done
+        unsigned d = ld_sc1_u32(done + img), spins = 0;
+        while (d < need) {
+          __builtin_amdgcn_s_sleep(2);
+          d = ld_sc1_u32(done + img);
+          if ((++spins & 1023u) == 0 &&
+              (__hip_atomic_load((gi32*)A.tfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+               spins > (1u << 26))) {
+            __hip_atomic_store((gi32*)A.tfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            t = total;
+            break;
+          }
+        }
+        if (t < total) {
+          if (d & kDoneStop) {
+            skip = 1;  // stopped: nothing of this image is read or written
+          } else {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+        }
+      }
+      s_task = t;
+      s_skip = skip;
+    }
+    __syncthreads();
+    const unsigned t = s_task;
+    const bool skip = s_skip != 0;
+    __syncthreads();  // s_task is rewritten by lane 0 only after every wave has read it
+    if (t >= total) break;
+    if (skip) continue;
+    const int img = A.img0 + (int)(t % nimg);
+    persist_dir<V>(img);
+    __syncthreads();  // rows of d and the direction scalars complete
+    persist_col_a(img);
+    persist_ls<K, MODE, ADAPT, V>(img);
+    __syncthreads();  // the accepted step and AT's columns complete
+    persist_bb<V>(img);
+    // publish iteration k of img: every wave's stores drained, then lane 0
+    // releases at agent scope and stores the flag (sc1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned k = t / nimg + 1;
+      const unsigned flag = A.st[img].stop ? (kDoneStop | k) : k;  // lane 0 is bb's leader
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store((gu32*)(done + img), flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// The persistent kernel for a trial width / objective mode (the same choice as
+// ls_kernel); nullptr where no persistent build exists (the phase kernels run).
+template <class V>
+inline const void* persist_kernel(int K, int mode, bool adapt) {
+  if (adapt) return (const void*)k_persist<1, -1, true, V>;
+  if (K > 2) K = 2;
+  if (mode == -1) return (const void*)k_persist<2, -1, false, V>;
+  if (mode == 0) return K == 1 ? (const void*)k_persist<1, 0, false, V>
+                               : (const void*)k_persist<2, 0, false, V>;
+  if (mode == 4) return K == 1 ? (const void*)k_persist<1, 4, false, V>
+                               : (const void*)k_persist<2, 4, false, V>;
+  return K == 1 ? (const void*)k_persist<1, 3, false, V> : (const void*)k_persist<2, 3, false, V>;
+}
+template <class V>
+inline void persist_kernels(std::vector<const void*>& f) {
+  for (int adapt = 0; adapt < 2; ++adapt)
+    for (int mode : {-1, 0, 3, 4})
+      for (int K : {1, 2}) f.push_back(persist_kernel<V>(K, mode, adapt != 0));
+}
+template <class V>
+inline hipError_t launch_persist_t(const SolveArgs& a, int K, size_t lds, hipStream_t s,
+                                   unsigned* queue, unsigned* done, int grid) {
+  const bsgp_params& P = a.prm;
+  const bool adapt = P.adapt_beta && P.variant == BSGP_VARIANT_BETA;
+  const bool special = a.in.beta0 ? !P.beta0_general : (P.betaParam == 0.0 || P.betaParam == 1.0);
+  const int mode = P.variant == BSGP_VARIANT_KL ? 0 : special ? -1 : P.gn_f32 ? 4 : 3;
+  SolveArgs aa = a;
+  void* args[] = {&aa, &queue, &done};
+  return hipLaunchKernel(persist_kernel<V>(K, mode, adapt), dim3(grid), dim3(kBlock), args, lds, s);
 }
 
 // ---------------------------------------- kernel: per-iteration tracking

@@ -406,6 +406,7 @@ hipError_t set_solver_lds_limit(size_t bytes) {
   solver_kernels<true, double>(fns);
   solver_kernels_f32(fns, false);
   solver_kernels_f32(fns, true);
+  persist_kernels_all(fns);
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return e;

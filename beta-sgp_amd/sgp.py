@@ -25,9 +25,10 @@ revert-to-previous-iterate on stop (sgp.py:424-425) and the returned tuple
 (SGP_reconstructed_images/, sgp.py:223-231, 416-422) from device snapshots of
 every iterate; ``errflag=True`` (``sgp`` only, as in the reference) returns
 the per-iteration error as the fifth element (sgp.py:240-257, 394-396).
-A float32 image is scaled in float32 on the host and solved with the
-reference's float32 arithmetic reproduced on the device (numpy 1.x rules;
-include/bsgp.h ``gn_f32``).
+A float32 image is solved with the reference's float32 arithmetic
+reproduced on the device, its float32 prelude (scaling, null-pixel fill,
+start, flux) included (numpy 1.x rules; include/bsgp.h ``gn_f32``), in the
+single-image drop-in and in the batched calls alike.
 
 Deliberate differences: a plain Python float ``bkg`` is
 accepted (the reference crashes on ``bkg.flatten()``); errflag at MAXIT
@@ -72,6 +73,7 @@ STREAMS_DEFAULT = 8 if _hw_queues() >= 8 else 4
 TEAM_DEFAULT = 0  # workgroups per image: 0 = auto (spread small batches over the CUs)
 PROJ_CACHE_DEFAULT = 1  # projectDF evaluations inside a known root bracket read a pixel list
 GN_COMPACT_DEFAULT = 1  # f32-exact observed images stored in f32 (bit-identical results)
+PERSIST_DEFAULT = 0  # one-workgroup batches: all iterations in one persistent launch
 
 
 # ------------------------------------------------------------------ helpers
@@ -155,6 +157,23 @@ def _prelude_host(gn, bkg, init_recon, flux, stop_criterion, scale_data):
     return gn, bkf, x, float(scaling), float(tol4), flux_s
 
 
+def _f32_on_device(init_recon, flux, bkg):
+    """A float32 image's prelude (sgp.py:620-666) runs on the device
+    (include/bsgp.h gn_f32 with scale_data 0/1) unless numpy would compute part
+    of it in float32 from the background too: a float32 (or integer)
+    background, or init_recon 3 without a flux and with a scalar background
+    (np.sum(gn - bkg) of a float32 array, sgp.py:629).  Those few cases keep
+    the host prelude (_prelude_host)."""
+    b = np.asarray(bkg)
+    if not (b.dtype.kind == "f" and b.dtype.itemsize == 8):  # any byte order
+        return False
+    return not (init_recon == 3 and flux is None and b.size == 1)
+
+
+def _flux_is_f32(flux):
+    return flux is not None and np.asarray(flux).dtype == np.float32
+
+
 def _gn_scaled_host(gn, scale_data):
     """The scaled, null-pixel-fixed float64 image of sgp.py:193-204, for the
     FITS files of save=True only (orig.fits, res_k.fits)."""
@@ -170,7 +189,7 @@ def _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, 
             alpha_max, M_alpha, tau, M, max_projs, verbose, ccd_sat_level, scale_data,
             tol_convergence, adapt_beta=False, betaParam=1.005, lr=1e-3, lr_exp_param=0.1,
             schedule_lr=False, bkg_is_map=False, ls_spec=None, ls_series=None, streams=None,
-            team=None, proj_cache=None, gn_compact=None, betaParams=None):
+            team=None, proj_cache=None, gn_compact=None, betaParams=None, persistent=None):
     p = _B.Params()
     p.variant = variant
     p.init_recon = int(init_recon)
@@ -199,6 +218,7 @@ def _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, 
     p.proj_cache = PROJ_CACHE_DEFAULT if proj_cache is None else int(bool(proj_cache))
     p.gn_compact = GN_COMPACT_DEFAULT if gn_compact is None else int(bool(gn_compact))
     p.gn_f32 = 0
+    p.persistent = PERSIST_DEFAULT if persistent is None else int(bool(persistent))
     if betaParams is not None:
         b0 = np.asarray(betaParams, dtype=np.float64)
         p.beta0_general = int(bool(np.all((b0 != 0.0) & (b0 != 1.0))))
@@ -303,7 +323,19 @@ def _run(variant, gn, psf, bkg, init_recon, proj_type, stop_criterion, MAXIT, ga
     x0 = None
     fl = None if flux is None else np.array([float(flux)])
     f32 = gn.dtype.kind == "f" and gn.dtype.itemsize == 4
-    if f32:
+    dev32 = f32 and _f32_on_device(init_recon, flux, b if bkg_is_map else bkg)
+    if dev32:
+        # float32 image: the device runs the reference's float32 prelude
+        # (scaling, null-pixel fill, start, flux; include/bsgp.h ABI 3)
+        g = np.asarray(gn, dtype=np.float64)  # the float32 values, exact
+        bk = b
+        prm.gn_f32 = 1
+        prm.scale_data = 1 if scale_data else 0
+        prm.flux_f32 = int(_flux_is_f32(flux))
+        if init_recon == 1:
+            np.random.seed(42)
+            x0 = np.random.randn(*gn.shape)
+    elif f32:
         # the reference computes in the image's float32 (sgp.py:193-211): scale
         # on the host in float32, and let the device reproduce the float32
         # parts of the beta objective (include/bsgp.h gn_f32)
@@ -323,7 +355,7 @@ def _run(variant, gn, psf, bkg, init_recon, proj_type, stop_criterion, MAXIT, ga
         if init_recon == 1:
             np.random.seed(42)
             x0 = np.random.randn(*gn.shape)
-    plan = _B.get_plan(_shape[0], _shape[1], psf, mode)
+    _B.require_gpu()  # the product path runs on the device or not at all
     gd = _B.to_dev(np.asarray(g, dtype=np.float64).reshape(1, *_shape))
     bd = _B.to_dev(np.asarray(bk, dtype=np.float64).reshape((1, *_shape) if bkg_is_map else (1,)))
     fd = None if fl is None else _B.to_dev(fl)
@@ -331,8 +363,12 @@ def _run(variant, gn, psf, bkg, init_recon, proj_type, stop_criterion, MAXIT, ga
     od = None if not errflag else _B.to_dev(np.asarray(obj, dtype=np.float64).reshape(1, *_shape))
     gs = None
     if save:
-        gs = np.asarray(g, dtype=np.float64).reshape(-1) if f32 else _gn_scaled_host(g, scale_data)
-        _save_setup(np.asarray(g).reshape(-1) if f32 else gs, _shape)
+        g_f = g
+        if dev32:  # the scaled float32 image of the FITS files, restated on the host
+            g_f = _prelude_host(gn, b if bkg_is_map else np.asarray(bkg).reshape(()), init_recon,
+                                flux, stop_criterion, scale_data)[0]
+        gs = np.asarray(g_f, dtype=np.float64).reshape(-1) if f32 else _gn_scaled_host(g, scale_data)
+        _save_setup(np.asarray(g_f).reshape(-1) if f32 else gs, _shape)
     b0 = None
     if betas is not None:
         nb = len(betas)
@@ -340,7 +376,8 @@ def _run(variant, gn, psf, bkg, init_recon, proj_type, stop_criterion, MAXIT, ga
                           for t in (gd, bd, xd, od))
         fd = None if fd is None else fd.expand(nb).contiguous()
         b0 = _B.to_dev(np.asarray(betas, dtype=np.float64))
-    out = plan.solve(gd, bd, prm, flux=fd, x0=xd, obj=od, beta0=b0, want_iterates=bool(save))
+    with _B.lease_plan(_shape[0], _shape[1], psf, mode) as plan:
+        out = plan.solve(gd, bd, prm, flux=fd, x0=xd, obj=od, beta0=b0, want_iterates=bool(save))
     _B.torch.cuda.current_stream().synchronize()
     _B.check_status(out["counters"])
     if betas is not None:
@@ -358,8 +395,8 @@ def _run(variant, gn, psf, bkg, init_recon, proj_type, stop_criterion, MAXIT, ga
     times = out["times"][0, :it + 1].cpu().numpy()
     if verbose or stop_criterion in (1, 2, 3, 4):
         tol = tol_convergence
-        if stop_criterion == 4:
-            tol = 1 + 1 / np.mean(np.asarray(gn, dtype=np.float64))
+        if stop_criterion == 4:  # sgp.py:644, in the image's dtype
+            tol = 1 + 1 / float(np.mean(gn if f32 else np.asarray(gn, dtype=np.float64)))
         if stop_criterion == 2 and verbose:
             tol = tol * tol
         _write_log(stop_criterion, verbose, discr, out["crit"][0].cpu().numpy(),
@@ -466,12 +503,29 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
                  use_original_SGP_Afunction=True, adapt_beta=False, betaParam=1.005, lr=1e-3,
                  lr_exp_param=0.1, schedule_lr=False, ls_spec=None, ls_series=None,
                  streams=None, team=None, proj_cache=None, gn_compact=None,
-                 device_out=False, profile=False, storage="f64"):
+                 device_out=False, profile=False, storage="f64", gn_f32=None, save=False,
+                 errflag=False, obj=None, persistent=None):
     torch = _B.torch
+    if save or errflag:  # sgp()/sgp_betaDiv() keywords: per-image files / err arrays
+        raise ValueError("save / errflag are single-image options: use sgp / sgp_betaDiv")
     per_image = (psf.dim() if torch.is_tensor(psf) else np.ndim(psf)) == 3
     if not per_image:
         _check_psf(np.asarray(psf))
     _B.require_gpu()
+    # float32 images (the application's FITS data): the reference's float32
+    # prelude on the device, per image (include/bsgp.h gn_f32, ABI 3)
+    if gn_f32 is None:
+        gn_f32 = (gns.dtype == torch.float32) if torch.is_tensor(gns) else \
+            np.asarray(gns).dtype.kind == "f" and np.asarray(gns).dtype.itemsize == 4
+    if gn_f32:
+        f64b = (bkgs.dtype == torch.float64) if torch.is_tensor(bkgs) else \
+            (np.asarray(bkgs).dtype.kind == "f" and np.asarray(bkgs).dtype.itemsize == 8)
+        bnd = bkgs.dim() if torch.is_tensor(bkgs) else np.ndim(bkgs)
+        if not f64b or (init_recon == 3 and flux is None and bnd <= 1):
+            raise ValueError("float32 images in a batch need float64 backgrounds, and a flux for "
+                             "init_recon=3 with scalar backgrounds (numpy computes those parts "
+                             "in float32 from the background; solve such images one at a time "
+                             "with sgp_betaDiv / sgp)")
     if torch.is_tensor(gns):
         gns = gns.to(device="cuda", dtype=torch.float64).contiguous()
     else:
@@ -487,22 +541,33 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
                   scale_data, tol_convergence, adapt_beta=adapt_beta, betaParam=betaParam, lr=lr,
                   lr_exp_param=lr_exp_param, schedule_lr=schedule_lr, bkg_is_map=bkg_is_map,
                   ls_spec=ls_spec, ls_series=ls_series, streams=streams,
-                  team=team, proj_cache=proj_cache, gn_compact=gn_compact, betaParams=betaParams)
+                  team=team, proj_cache=proj_cache, gn_compact=gn_compact, betaParams=betaParams,
+                  persistent=persistent)
+    if gn_f32:
+        prm.gn_f32 = 1
+        prm.scale_data = 1 if scale_data else 0
+        prm.flux_f32 = int(_flux_is_f32(flux) if not torch.is_tensor(flux)
+                           else flux.dtype == torch.float32)
     x0 = None
     if init_recon == 1:
         np.random.seed(42)
         x0 = _B.to_dev(np.broadcast_to(np.random.randn(H, W), (Bn, H, W)))
     b0 = None if betaParams is None else _B.to_dev(np.broadcast_to(
         np.asarray(betaParams, dtype=np.float64), (Bn,)))
-    fl = None if flux is None else _B.to_dev(np.broadcast_to(np.asarray(flux, dtype=np.float64),
-                                                            (Bn,)))
+    if flux is None:
+        fl = None
+    elif torch.is_tensor(flux):
+        fl = flux.to(device="cuda", dtype=torch.float64).reshape(-1).expand(Bn).contiguous()
+    else:
+        fl = _B.to_dev(np.broadcast_to(np.asarray(flux, dtype=np.float64), (Bn,)))
     if per_image:  # psf [B, kh, kw]: image i uses psf[i] (each checked as sgp.py:97-102)
         if len(psf) != Bn:
             raise ValueError("one PSF per image: psf must be [B, kh, kw]")
         plan = _B.per_image_plan(H, W, psf, mode, storage=storage)
+        out = plan.solve(gns, bkgs, prm, flux=fl, x0=x0, beta0=b0, profile=profile)
     else:
-        plan = _B.get_plan(H, W, np.asarray(psf), mode, storage=storage)
-    out = plan.solve(gns, bkgs, prm, flux=fl, x0=x0, beta0=b0, profile=profile)
+        with _B.lease_plan(H, W, np.asarray(psf), mode, storage=storage) as plan:
+            out = plan.solve(gns, bkgs, prm, flux=fl, x0=x0, beta0=b0, profile=profile)
     if device_out:
         return out
     prof = {k: out.pop(k) for k in ("kernel_ms", "launches") if k in out}
@@ -561,6 +626,11 @@ def _solve_sharded(variant, gns, psf, bkgs, devices, betaParams=None, flux=None,
     Bn = gns.shape[0]
     if kw.get("device_out"):
         raise ValueError("devices=... returns host arrays (device_out is per device)")
+    if len(set(devices)) < len(list(devices)):
+        # several shards on one GPU run concurrently: team solves size their
+        # teams for the whole device and spin on co-resident members, so
+        # shards that share a GPU use one workgroup per image
+        kw["team"] = 1
     per_image_psf = (psf.dim() if _B.torch.is_tensor(psf) else np.ndim(psf)) == 3
 
     def work(dev, lo, hi):
@@ -613,13 +683,33 @@ def app_beta_candidates(seeds=APP_BETA_SEEDS, loc=1.0, scale=0.05):
     return out
 
 
+def argmin_strict(scores):
+    """The application's choice among the candidates
+    (application_sgp_subdivisions.py:78-99, application_sgp_star_stamps.py:
+    75-98): running minimum from +inf, a candidate wins only with a score
+    strictly below every earlier one, so the first of equal scores wins and a
+    NaN score never does.  None when no score is below +inf (the reference is
+    then left with best_beta_init = None)."""
+    best, low = None, np.inf
+    for i, v in enumerate(scores):
+        if v < low:
+            low, best = v, i
+    return best
+
+
 def sgp_betaDiv_multistart(gn, psf, bkg, betas=None, score=None, final_solve=True, devices=None,
                            **kwargs):
-    """The beta search of application_sgp_subdivisions.py:69-107 as two
-    launches: every candidate initial beta (default: the application's five
-    seeds) is solved in ONE batched launch, the host takes the argmin of
-    ``score(x)`` over the candidates, and -- as the application does -- the
-    image is solved once more with the best initial beta.
+    """The beta search of application_sgp_subdivisions.py:69-107 in ONE
+    batched launch: every candidate initial beta (default: the application's
+    five seeds) is solved together, and the host picks the best candidate by
+    ``score(x)`` with the application's strict running minimum
+    (:func:`argmin_strict`).
+
+    The application then solves the image once more with the best initial
+    beta (:100-107).  The reference is deterministic, so that run repeats the
+    best candidate's run exactly; here the candidate's result is returned
+    instead of solving again (with final_solve=True the final run's two
+    printed lines, sgp.py:892-893, are repeated for it).
 
     ``score`` is the application's criterion, the photometric flux fractional
     difference 1 - sum(segment_flux(x)) / sum(segment_flux(gn)) (:92-99); it
@@ -629,9 +719,10 @@ def sgp_betaDiv_multistart(gn, psf, bkg, betas=None, score=None, final_solve=Tru
     sgp_betaDiv's keyword arguments.  ``devices=[...]`` spreads the
     candidates over GPUs (one batched launch per GPU).
 
-    Returns (x, iters, discr, times, None) of the final solve and a dict with
-    "betas", "scores", "best_beta" and "candidates" (each candidate's
-    (x, iters, discr, times, None))."""
+    Returns (x, iters, discr, times, None) of the best candidate and a dict
+    with "betas", "scores", "best_beta", "best", "beta_final" (the final beta
+    of every candidate) and "candidates" (each candidate's (x, iters, discr,
+    times, None))."""
     betas = list(app_beta_candidates() if betas is None else betas)
     kw = dict(kwargs)
     kw.pop("betaParam", None)
@@ -648,14 +739,17 @@ def sgp_betaDiv_multistart(gn, psf, bkg, betas=None, score=None, final_solve=Tru
     args.update(kw)
     if args["save"]:
         raise ValueError("save=True writes one set of files per solve: use sgp_betaDiv")
+    shared = devices is not None and len(set(devices)) < len(list(devices))
+
     def work(dev, lo, hi):
+        extra = dict(team=1) if shared else {}  # shards sharing a GPU: no spinning teams
         return _run(_B.BSGP_VARIANT_BETA, gn, psf, bkg, args["init_recon"], args["proj_type"],
                     args["stop_criterion"], args["MAXIT"], args["gamma"], args["beta"],
                     args["alpha"], args["alpha_min"], args["alpha_max"], args["M_alpha"],
                     args["tau"], args["M"], args["max_projs"], False, None, args["verbose"],
                     args["flux"], args["ccd_sat_level"], args["scale_data"], False,
                     args["tol_convergence"], args["use_original_SGP_Afunction"],
-                    dict(bkw, betaParam=betas[lo]), betas=betas[lo:hi])
+                    dict(bkw, betaParam=betas[lo], **extra), betas=betas[lo:hi])
 
     if devices is None:
         runs = work(None, 0, len(betas))
@@ -663,9 +757,13 @@ def sgp_betaDiv_multistart(gn, psf, bkg, betas=None, score=None, final_solve=Tru
         runs = [r for part in on_devices(devices, len(betas), work) for r in part]
     cands = [(x, it, d, t, None) for x, it, d, t, _ in runs]
     scores = [float(score(c[0])) if score is not None else float(c[2][-1]) for c in cands]
-    best = int(np.argmin(scores))
-    info = {"betas": betas, "scores": scores, "best_beta": betas[best], "candidates": cands}
-    if not final_solve:
-        return cands[best], info
-    final = sgp_betaDiv(gn, psf, bkg, betaParam=betas[best], **bkw, **kw)
-    return final, info
+    best = argmin_strict(scores)
+    if best is None:
+        raise ValueError(f"no candidate has a finite score below +inf: {scores} (the reference "
+                         "would call sgp_betaDiv with betaParam=None)")
+    info = {"betas": betas, "scores": scores, "best_beta": betas[best], "best": best,
+            "beta_final": [r[4]["beta"] for r in runs], "candidates": cands}
+    if final_solve:
+        print(f'Beta parameter in beta-divergence (final value): {runs[best][4]["beta"]}')
+        print(f'No. of iterations: {cands[best][1]}')
+    return cands[best], info

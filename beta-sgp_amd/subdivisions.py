@@ -116,6 +116,11 @@ def sgp_subdivisions(image, psf, bkg, subdiv_shape=(256, 256), overlap=32, betaP
     unless device_out."""
     import sgp
     torch = _B.torch
+    # a float32 field (the application's FITS data) keeps the reference's
+    # float32 arithmetic per tile (sgp.py:648-666; include/bsgp.h gn_f32)
+    f32 = (image.dtype == torch.float32) if torch.is_tensor(image) else \
+        (np.asarray(image).dtype.kind == "f" and np.asarray(image).dtype.itemsize == 4)
+    sgp_kwargs.setdefault("gn_f32", bool(f32))
     img = _field(image)
     H, W = img.shape
     boxes = subdivision_boxes((H, W), subdiv_shape, overlap)
@@ -136,3 +141,73 @@ def sgp_subdivisions(image, psf, bkg, subdiv_shape=(256, 256), overlap=32, betaP
     _B.check_status(out["counters"])
     return mosaic.cpu().numpy(), foot.cpu().numpy(), \
         {k: (v.cpu().numpy() if v is not None else None) for k, v in out.items()}
+
+
+def sgp_subdivisions_multistart(image, psf, bkg, betas=None, score=None, subdiv_shape=(256, 256),
+                                overlap=32, **sgp_kwargs):
+    """The application's beta search for every subdivision of a field at once
+    (application_sgp_subdivisions.py:69-107 per tile): the (tile x candidate)
+    product -- n tiles x K initial betas (default: the application's five
+    seeds) -- is ONE batched solve, image t*K + k being tile t with beta k;
+    each tile keeps the candidate its score ranks best with the application's
+    strict running minimum (sgp.argmin_strict), and the mosaic is co-added
+    from those.  The application's final re-solve with the best beta repeats
+    that candidate's run exactly (the reference is deterministic), so it is
+    not run again.
+
+    ``score(x, tile)`` (host arrays of one candidate and its observed tile)
+    stands in for the application's photometric score (photutils, absent
+    here); without one the final discrepancy ranks the candidates.  ``psf``,
+    ``bkg`` and the keyword arguments as in :func:`sgp_subdivisions`.
+    Returns (mosaic, footprint, info): info holds the boxes, "betas",
+    "scores" [n, K], "best" [n] (candidate index per tile), "best_beta" [n],
+    and the solve outputs of the chosen candidates ("x", "iters", "discr",
+    "beta_final")."""
+    import sgp
+    torch = _B.torch
+    betas = list(sgp.app_beta_candidates() if betas is None else betas)
+    K = len(betas)
+    f32 = (image.dtype == torch.float32) if torch.is_tensor(image) else \
+        (np.asarray(image).dtype.kind == "f" and np.asarray(image).dtype.itemsize == 4)
+    sgp_kwargs.setdefault("gn_f32", bool(f32))
+    img = _field(image)
+    H, W = img.shape
+    boxes = subdivision_boxes((H, W), subdiv_shape, overlap)
+    n = len(boxes)
+    tiles = extract_tiles(img, boxes, subdiv_shape)
+    b = np.asarray(bkg) if not torch.is_tensor(bkg) else bkg
+    if (torch.is_tensor(b) and b.dim() == 2) or (not torch.is_tensor(b) and b.ndim == 2):
+        bk = extract_tiles(b, boxes, subdiv_shape).repeat_interleave(K, dim=0)
+    else:
+        bk = torch.full((n * K,), float(b), dtype=torch.float64, device="cuda")
+    if hasattr(psf, "stamps"):
+        psf = psf.stamps(tile_centres(boxes), normalize=True, device_out=True)
+    if (psf.dim() if torch.is_tensor(psf) else np.ndim(psf)) == 3:
+        pt = psf if torch.is_tensor(psf) else _B.to_dev(np.asarray(psf, dtype=np.float64))
+        psf = pt.repeat_interleave(K, dim=0)
+    gns = tiles.repeat_interleave(K, dim=0)
+    out = sgp.sgp_betaDiv_batch(gns, psf, bk, betaParams=np.tile(np.asarray(betas, float), n),
+                                **sgp_kwargs)
+    t_host = tiles.cpu().numpy()
+    scores = np.empty((n, K))
+    for t in range(n):
+        for k in range(K):
+            i = t * K + k
+            it = int(out["iters"][i])
+            scores[t, k] = (float(score(out["x"][i], t_host[t])) if score is not None
+                            else float(out["discr"][i, it]))
+    best = []
+    for t in range(n):
+        j = sgp.argmin_strict(scores[t])
+        if j is None:
+            raise ValueError(f"tile {t}: no candidate scores below +inf ({scores[t]})")
+        best.append(j)
+    best = np.asarray(best)
+    pick = np.arange(n) * K + best
+    xs = out["x"][pick]
+    mosaic, foot = coadd_tiles(xs, boxes, (H, W))
+    info = {"boxes": boxes, "betas": betas, "scores": scores, "best": best,
+            "best_beta": np.asarray(betas)[best], "x": xs, "iters": out["iters"][pick],
+            "discr": out["discr"][pick], "beta_final": out["beta_final"][pick]}
+    torch.cuda.current_stream().synchronize()
+    return mosaic.cpu().numpy(), foot.cpu().numpy(), info

@@ -69,7 +69,9 @@ typedef struct {
   int32_t has_sat;
   int32_t scale_data;     /* 0 none, 1 scaling = max(gn) on device (sgp.py:193-199),
                              2 inputs already scaled by the caller in their own dtype:
-                             gn, bkg, x0 are used as given (x0 required)          */
+                             gn, bkg, x0 are used as given (x0 required); with
+                             gn_f32, 0 and 1 run the float32 prelude on the device
+                             (see below)                                           */
   int32_t verbose;        /* only changes tol**2 for stop_criterion 2 (sgp.py:291-294) */
   int32_t adapt_beta;
   int32_t schedule_lr;
@@ -100,7 +102,24 @@ typedef struct {
                              scaling matrix clips to float32 bounds (sgp.py:726-729). */
   int32_t beta0_general;  /* 1: every in->beta0[b] is neither 0 nor 1, so a batch with
                              per-image betas can use the general-beta kernels */
+  int32_t flux_f32;       /* gn_f32 with scale_data 0/1: in->flux holds numpy float32
+                             values, divided by the scaling in float32 (sgp.py:666) */
+  int32_t persistent;     /* 1: one-workgroup images (team 1, per-wave transforms, no
+                             err / x_iter) run every iteration in ONE persistent launch
+                             that dequeues (iteration, image) tasks; the same device
+                             code per iteration, bit-identical results.  0: one launch
+                             per phase and iteration on sub-batch streams */
 } bsgp_params;
+/* gn_f32 with scale_data 0 or 1 (ABI 3): the float32 prelude of sgp.py:620-666
+ * runs on the device.  in->gn holds the raw float32 image values (exact in
+ * float64), in->bkg float64 backgrounds, in->flux the raw provided flux; the
+ * device takes scaling = max(gn), gn/scaling and (init_recon 2) x/scaling in
+ * float32, the null-pixel fill rounded to float32, stop rule 4's 1 + 1/mean(gn)
+ * from numpy's float32 mean, and init_recon 3's flat start rounded to float32,
+ * as numpy 1.x evaluates them for a float32 image (bkg/scaling, a float64
+ * flux/scaling and x0/scaling stay float64).  Not covered (the caller scales):
+ * float32 backgrounds, and init_recon 3 without a flux and with a scalar bkg
+ * (numpy sums that start in float32). */
 
 /* Storage of the per-image iteration vectors (bsgp_plan_create). */
 #define BSGP_STORAGE_F64 0
@@ -124,7 +143,10 @@ typedef struct {
   double* discr;       /* [B][MAXIT1] discrepancy 2/N*scaling*f (sgp.py:276,392)  */
   double* times;       /* [B][MAXIT1] seconds since solve start (sgp.py:391), may be NULL */
   double* crit;        /* [B][MAXIT1] stop-rule value per iteration, may be NULL  */
-  int32_t* flags;      /* [B][MAXIT1] bit0: fv >= fr warning (sgp.py:351), may be NULL */
+  int32_t* flags;      /* [B][MAXIT1] bit0: fv >= fr warning (sgp.py:351, 803);
+                          bits 8..23: line-search trials of iteration k (the
+                          betaDiv calls of sgp.py:782 / objective evaluations of
+                          :334 in iteration k); may be NULL */
   double* beta_final;  /* [B] final betaParam (sgp.py:892), may be NULL           */
   int64_t* counters;   /* [B][8]: proj evals E_p, line-search trials E_ls,
                           line-search passes over the image, status bits (1: line
@@ -159,8 +181,9 @@ int bsgp_solve_device(bsgp_plan plan, int32_t B, const bsgp_params* params,
 
 /* Measurement: bsgp_solve_device on the one stream `stream` (params->streams is
  * taken as 1) with a HIP event recorded around every kernel launch;
- * kernel_ms[k] and launches[k] (k < 5) receive the summed span and the launch
- * count of kernel class k: 0 setup, 1 k_dir, 2 k_col (A and AT), 3 k_ls, 4 k_bb.
+ * kernel_ms[k] and launches[k] (k < 6) receive the summed span and the launch
+ * count of kernel class k: 0 setup, 1 k_dir, 2 k_col (A and AT), 3 k_ls, 4 k_bb,
+ * 5 k_persist (the persistent solver: every iteration in one launch).
  * Synchronous (waits for the solve). */
 int bsgp_solve_profiled(bsgp_plan plan, int32_t B, const bsgp_params* params,
                         const bsgp_inputs* in, const bsgp_outputs* out, void* stream,

@@ -35,6 +35,38 @@ def ngc():
     return d["gn"], d["psf"], d["bg"][0][0], d["obj"]
 
 
+STAGNATION_TRIALS = 20  # accepted step 0.4**19 ~ 3e-8: below the objective's rounding floor
+
+
+def compare_trials(dev, ref, what=""):
+    """Line-search trials per iteration, engine (or oracle) vs the reference.
+
+    An iteration whose accepted step lies above the objective's rounding
+    floor (the reference needed fewer than STAGNATION_TRIALS trials) must
+    take exactly the reference's trials.  In a stagnating iteration the
+    Armijo test (sgp.py:784) compares f(lam) - fr ~ lam*gd ~ 1e-9*|gd| with
+    differences at the rounding level of f, so which of the trials 20..32 is
+    accepted depends on the last bits of the sums: the numpy restatement of
+    the reference (oracle/sgp_oracle.py, same formulas, another FFT and
+    numpy version) already differs from the reference there in about half of
+    those iterations while its iterates agree to 1e-10.  There both must
+    stagnate (>= STAGNATION_TRIALS trials, so the accepted step moves x by
+    less than 3e-8 of d).  Returns the 1-based stagnating iterations whose
+    counts differ, so callers can report them."""
+    dev = np.asarray(dev, dtype=np.int64)
+    ref = np.asarray(ref, dtype=np.int64)
+    assert dev.shape == ref.shape, (what, dev.shape, ref.shape)
+    live = ref < STAGNATION_TRIALS
+    bad = np.nonzero(live & (dev != ref))[0]
+    assert bad.size == 0, (f"{what}: trials differ in non-stagnating iterations {list(bad + 1)}: "
+                           f"got {list(dev[bad])}, reference {list(ref[bad])}")
+    stag = ~live
+    lost = np.nonzero(stag & (dev < STAGNATION_TRIALS))[0]
+    assert lost.size == 0, (f"{what}: iterations {list(lost + 1)} stagnate in the reference "
+                            f"({list(ref[lost])} trials) but not here ({list(dev[lost])})")
+    return list(np.nonzero(stag & (dev != ref))[0] + 1)
+
+
 def app_case(name):
     """Inputs + reference outputs of one application-path fixture
     (tests/golden/make_golden.py app): the raw big-endian float32 image as

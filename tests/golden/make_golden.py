@@ -119,6 +119,42 @@ def run_quiet(fn, *a, **k):
         return fn(*a, **k)
 
 
+def run_counted(sgp, fn, *a, **k):
+    """run_quiet(getattr(sgp, fn), ...) that also returns the reference's
+    line-search trials of every iteration: the calls of the module-level
+    betaDiv (restoration/sgp.py:782) between two calls of the module-level
+    projectDF (:763, once per iteration with proj_type=1).  The reference is
+    not modified: its two globals are wrapped for the duration of the call.
+    The first segment (setup: the initial projectDF :699, betaDiv :709) is
+    dropped."""
+    seq = []
+    ob, op = sgp.betaDiv, sgp.projectDF
+
+    def b(*x, **y):
+        seq.append("b")
+        return ob(*x, **y)
+
+    def p(*x, **y):
+        seq.append("p")
+        return op(*x, **y)
+
+    sgp.betaDiv, sgp.projectDF = b, p
+    try:
+        out = run_quiet(getattr(sgp, fn), *a, **k)
+    finally:
+        sgp.betaDiv, sgp.projectDF = ob, op
+    trials, cur = [], None
+    for s in seq:
+        if s == "p":
+            if cur is not None:
+                trials.append(cur)
+            cur = 0
+        else:
+            cur += 1
+    trials.append(cur)
+    return out, np.array(trials[1:], dtype=np.int32)
+
+
 # --------------------------------------------------------------------------- circular
 def make_circular(solves_too=True):
     from scipy.io import loadmat
@@ -344,6 +380,65 @@ def make_linear():
         print(f"{name:18s} {fn:12s} iters={it:3d} discr0={discr[0]:.10f} discrN={discr[-1]:.10f}")
 
 
+def make_long():
+    """BASELINE config C3's timed workload to its full MAXIT = 100 (SURVEY §8d:
+    256x256, 25x25 PSF, linear A, beta = 1.05, projection, stop rule 1) for the
+    lin256_beta image (seed 0) and two more seeds of the same generator, plus
+    the stop-3 (tol 1e-5) variant on seed 0.  From iteration ~40 on these
+    runs stagnate at 20-32 line-search trials per iteration, the regime the
+    engine evaluates with its moment series; the trial count of every
+    iteration is recorded (run_counted) so the device's per-iteration count
+    can be compared with the reference's."""
+    sgp, fcp = import_reference(need_astropy=True)
+    app = dict(gamma=1e-4, beta=0.4, alpha_min=1e-5, alpha_max=1e5, alpha=10.0, M_alpha=3,
+               tau=0.5, M=1, proj_type=1, max_projs=1000, init_recon=2, ccd_sat_level=65000.0,
+               scale_data=True, use_original_SGP_Afunction=False, betaParam=1.05, lr=1e-3,
+               lr_exp_param=0.1, schedule_lr=True, adapt_beta=False)
+    runs = {"c3long_s0": (0, dict(app, stop_criterion=1, MAXIT=100)),
+            "c3long_s1": (1, dict(app, stop_criterion=1, MAXIT=100)),
+            "c3long_s2": (2, dict(app, stop_criterion=1, MAXIT=100)),
+            "c3stop3_s0": (0, dict(app, stop_criterion=3, MAXIT=500, tol_convergence=1e-5))}
+    for name, (seed, kw) in runs.items():
+        gn, psf, _ = synth_field(256, 25, 200, seed=seed)
+        (x, it, discr, _, _), trials = run_counted(sgp, "sgp_betaDiv", gn, psf, np.float64(100.0),
+                                                   **kw)
+        assert len(trials) == it, (len(trials), it)
+        np.savez_compressed(os.path.join(OUT, f"ref_{name}.npz"), gn=gn.astype(np.int32),
+                            psf=psf, bkg=np.asarray(100.0), flux=np.asarray(np.nan), x=x,
+                            iters=it, discr=discr, trials=trials, seed=seed, kwargs=repr(kw),
+                            fn="sgp_betaDiv")
+        stag = int(np.sum(trials >= 20))
+        print(f"{name:12s} iters={it:3d} trials={trials.sum()} stagnating(>=20)={stag} "
+              f"discrN={discr[-1]:.12f}")
+
+
+def make_c4():
+    """BASELINE config C4's field (2048x2048, 5000 stars, 64x64
+    Gaussian PSF embedded at the centre, circular A, beta = 1.05, projection)
+    to MAXIT = 20 with the reference (py3.10 / numpy 2.2, circular A needs no
+    astropy).  The input is rebuilt by oracle/cpu_bench.make_stamp(0, 2048,
+    64, 5000, circular=True) wherever the fixture is used, so only the
+    outputs are stored: the discrepancy and trial count of every iteration,
+    sum(x), the flux-weighted centroid, and four 64x64 windows of x."""
+    sgp, fcp = import_reference(need_astropy=False)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(OUT)), "oracle"))
+    import cpu_bench
+    gn, psf = cpu_bench.make_stamp(0, 2048, 64, 5000, circular=True)
+    kw = dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=20, alpha=10.0,
+              ccd_sat_level=65000.0, use_original_SGP_Afunction=True, schedule_lr=True,
+              adapt_beta=False, betaParam=1.05)
+    (x, it, discr, _, _), trials = run_counted(sgp, "sgp_betaDiv", gn, psf, np.float64(100.0),
+                                               **kw)
+    wins = np.array([[0, 0], [1000, 1000], [517, 1733], [1984, 64]], dtype=np.int32)
+    out = dict(iters=it, discr=discr, trials=trials, xsum=np.sum(x), x2=np.sum(x * x),
+               gn_sum=np.sum(gn), gn_x2=np.sum(gn * gn), wins=wins, kwargs=repr(kw),
+               fn="sgp_betaDiv")
+    for j, (r, c) in enumerate(wins):
+        out[f"win{j}"] = x[r:r + 64, c:c + 64]
+    np.savez_compressed(os.path.join(OUT, "ref_c4_maxit20.npz"), **out)
+    print("c4 iters", it, "trials", trials.sum(), "discrN", discr[-1])
+
+
 # --------------------------------------------------------------------------- errflag / save
 def make_errsave():
     """sgp(errflag=True, obj, save=True) and sgp_betaDiv(save=True) on the
@@ -478,6 +573,10 @@ if __name__ == "__main__":
                 make_app()
             elif which == "errsave":
                 make_errsave()
+            elif which == "long":
+                make_long()
+            elif which == "c4":
+                make_c4()
             else:
                 make_linear()
         finally:

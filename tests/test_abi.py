@@ -39,7 +39,7 @@ def test_library_exports_every_header_symbol():
 def test_ctypes_load_and_version():
     import _bsgp
     L = _bsgp.lib()
-    assert L.bsgp_abi_version() == 2
+    assert L.bsgp_abi_version() == 3
     for f in _bsgp.EXPORTED:
         assert hasattr(L, f)
     # argument validation runs on the host without a device

@@ -94,12 +94,114 @@ def test_multistart_candidates_match_reference(sgpmod):
         shift = konst_shift(gn, dict(kw, betaParam=betas[i]), fx)
         np.testing.assert_allclose(discr - shift, fx["discr"], rtol=1e-7)
     best = int(np.argmin([-np.max(c[0]) for c in info["candidates"]]))
-    assert info["best_beta"] == betas[best]
+    assert info["best_beta"] == betas[best] and info["best"] == best
+    # the application's final solve with the best beta repeats that
+    # candidate's run (the reference is deterministic): the candidate is returned
+    assert final is info["candidates"][best]
     x, it, discr, _, _ = final
     fx = target[best]
     assert it == int(fx["iters"]) and rel(x, fx["x"]) < SOLVE_RTOL
-    shift = konst_shift(gn, dict(kw, betaParam=betas[best]), fx)
-    np.testing.assert_allclose(discr - shift, fx["discr"], rtol=1e-7)
+
+
+def test_argmin_strict_is_the_applications_choice(sgpmod):
+    """application_sgp_subdivisions.py:78-99: running minimum from +inf with a
+    strict '<': first of equal scores, NaN never chosen, None if all NaN."""
+    a = sgpmod.argmin_strict
+    assert a([0.3, 0.1, 0.1, 0.2]) == 1
+    assert a([np.nan, 0.5, np.nan, 0.4]) == 3
+    assert a([np.nan, np.nan]) is None
+    assert a([np.inf, np.inf]) is None
+
+
+# ------------------------------------------ float32 images in the batched path
+def _app_batch_inputs(names):
+    cases = [app_case(n) for n in names]
+    gn = cases[0][0]
+    assert all(np.array_equal(c[0], gn) for c in cases)
+    return cases
+
+
+@pytest.mark.parametrize("names", [["app_beta0", "app_beta1", "app_beta2", "app_beta3",
+                                    "app_beta4"], ["app_beta2_flux32"], ["app_crop_beta"]])
+def test_batch_float32_images_match_reference_and_dropin(sgpmod, monkeypatch, names):
+    """The application's float32 FITS subdivision (and its non-contiguous crop,
+    and the float32 flux) through sgp_betaDiv_batch: the float32 prelude runs
+    on the device per image (include/bsgp.h gn_f32, ABI 3).  Every image
+    matches its reference run at the application tolerances, and is bitwise
+    equal to the single-image drop-in at the same team size."""
+    cases = _app_batch_inputs(names)
+    gn, psf, bkg, kw, fn, _ = cases[0]
+    kw = dict(kw)
+    kw.pop("betaParam", None)
+    flux = kw.pop("flux")
+    betas = [c[3]["betaParam"] for c in cases]
+    gns = np.stack([gn] * len(cases))  # float32 (big-endian) batch
+    assert gns.dtype.itemsize == 4
+    out = sgpmod.sgp_betaDiv_batch(gns, psf, bkg, betaParams=betas, flux=flux, team=1, **kw)
+    monkeypatch.setattr(sgpmod, "TEAM_DEFAULT", 1)
+    for i, (g, p, b, k, f, fx) in enumerate(cases):
+        it = int(out["iters"][i])
+        assert it == int(fx["iters"]), (names[i], it, int(fx["iters"]))
+        assert rel(out["x"][i], fx["x"]) < SOLVE_RTOL, (names[i], rel(out["x"][i], fx["x"]))
+        shift = konst_shift(g, k, fx)
+        np.testing.assert_allclose(out["discr"][i, :it + 1] - shift, fx["discr"], rtol=1e-7)
+        x1, it1, d1, _, _ = sgpmod.sgp_betaDiv(g, p, b, **k)
+        assert it1 == it
+        np.testing.assert_array_equal(x1, out["x"][i])
+        np.testing.assert_array_equal(d1, out["discr"][i, :it + 1])
+
+
+def test_subdivisions_float32_field_matches_reference(sgpmod):
+    """sgp_subdivisions on the application's float32 field, cut as one
+    375x375 subdivision: the tile chain keeps the float32 arithmetic and
+    reproduces the reference's run (ref_app_beta0)."""
+    import subdivisions
+    gn, psf, bkg, kw, fn, fx = app_case("app_beta0")
+    kw = dict(kw)
+    b0 = kw.pop("betaParam")
+    mosaic, foot, out = subdivisions.sgp_subdivisions(gn, psf, bkg, subdiv_shape=(375, 375),
+                                                      overlap=0, betaParams=[b0], team=1, **kw)
+    assert np.all(foot == 1)
+    assert int(out["iters"][0]) == int(fx["iters"])
+    assert rel(mosaic, fx["x"]) < SOLVE_RTOL, rel(mosaic, fx["x"])
+    it = int(fx["iters"])
+    np.testing.assert_allclose(out["discr"][0, :it + 1] - konst_shift(gn, dict(kw, betaParam=b0), fx),
+                               fx["discr"], rtol=1e-7)
+
+
+def test_subdivisions_multistart_tile_x_beta(sgpmod):
+    """(tile x beta) product in one launch with a per-tile strict argmin: each
+    tile's chosen candidate equals that tile solved alone with that beta, and
+    the mosaic is co-added from the chosen candidates."""
+    import subdivisions
+    gn, psf, bkg, kw, fn, _ = app_case("app_beta0")
+    kw = dict(kw)
+    kw.pop("betaParam")
+    kw.pop("flux")
+    kw["MAXIT"] = 12
+    betas = sgpmod.app_beta_candidates()
+
+    def score(x, tile):  # any function of the candidate and its tile
+        return float(np.abs(x - tile).sum())
+
+    field = np.ascontiguousarray(gn[:300, :300])
+    bmap = bkg[:300, :300]
+    mosaic, foot, info = subdivisions.sgp_subdivisions_multistart(
+        field, psf, bmap, betas=betas, score=score, subdiv_shape=(160, 160), overlap=20, team=1,
+        **kw)
+    boxes = info["boxes"]
+    assert info["scores"].shape == (len(boxes), 5)
+    np.testing.assert_array_equal(info["best"], np.argmin(info["scores"], axis=1))
+    for t, (x0, y0, x1, y1) in enumerate(boxes):
+        k = int(info["best"][t])
+        one = sgpmod.sgp_betaDiv_batch(field[None, y0:y1, x0:x1], psf, bmap[y0:y1, x0:x1],
+                                       betaParams=[betas[k]], team=1, **kw)
+        np.testing.assert_array_equal(one["x"][0], info["x"][t])
+    ref_m, ref_f, _ = subdivisions.sgp_subdivisions(field, psf, bmap, subdiv_shape=(160, 160),
+                                                    overlap=20, betaParams=info["best_beta"],
+                                                    team=1, **kw)
+    np.testing.assert_array_equal(foot, ref_f)
+    np.testing.assert_array_equal(mosaic, ref_m)
 
 
 def test_errflag_and_save_match_reference(sgpmod, tmp_path, monkeypatch):

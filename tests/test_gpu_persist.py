@@ -1,0 +1,84 @@
+"""The persistent task-queue solver (k_persist, include/bsgp.h `persistent`):
+one launch runs every iteration of every one-workgroup image by dequeuing
+(iteration, image) tasks, with an agent-scope hand-off between the workgroups
+that run consecutive iterations of an image.  It executes the same phase code
+as the per-iteration kernels, so results must be bit-identical to theirs --
+for every objective mode, both storages, data-dependent stop rules (tasks of
+stopped images are skipped) and batches larger than the resident workgroups
+(tasks wait for their predecessor iteration).  MI355X tests.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden, ref_kwargs
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("x", "iters", "discr", "crit", "flags", "beta_final")
+
+
+@pytest.fixture(scope="module")
+def sgpmod():
+    import _bsgp
+    _bsgp.require_gpu()
+    import sgp
+    return sgp
+
+
+def both(fn, *a, **kw):
+    p0 = fn(*a, persistent=0, **kw)
+    p1 = fn(*a, persistent=1, **kw)
+    for k in KEYS:
+        if p0.get(k) is not None:
+            np.testing.assert_array_equal(p1[k], p0[k], err_msg=k)
+    np.testing.assert_array_equal(p1["counters"][:, :3], p0["counters"][:, :3])
+    np.testing.assert_array_equal(p1["counters"][:, 4:], p0["counters"][:, 4:])
+    assert np.all(p1["counters"][:, 3] == 0)
+    return p1
+
+
+@pytest.mark.parametrize("case", ["beta", "kl", "adapt", "beta1", "f32storage"])
+def test_persistent_bitwise_equal_to_phase_kernels(sgpmod, case):
+    fx = golden("ref_lin64_beta.npz")
+    gn = fx["gn"].astype(np.float64)
+    gns = np.stack([np.roll(gn, 5 * i, 1) for i in range(6)])
+    kw = dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=12, alpha=10.0,
+              ccd_sat_level=65000.0, use_original_SGP_Afunction=False, schedule_lr=True, team=1)
+    if case == "kl":
+        both(sgpmod.sgp_batch, gns, fx["psf"], 100.0, **kw)
+        return
+    betas = [1.05, 0.97, 1.02, 0.99, 1.08, 1.01]
+    if case == "beta1":
+        betas = [1.0] * 6
+    extra = dict(adapt_beta=case == "adapt", storage="f32" if case == "f32storage" else "f64")
+    both(sgpmod.sgp_betaDiv_batch, gns, fx["psf"], 100.0, betaParams=betas, **kw, **extra)
+
+
+def test_persistent_stop3_matches_reference(sgpmod):
+    """Stop rule 3 inside the persistent launch (no host polling): the
+    reference's stop-3 run of the timed workload, and bitwise the phase
+    kernels, in a batch whose images stop at different iterations."""
+    fx = golden("ref_c3stop3_s0.npz")
+    kw = ref_kwargs(fx)
+    g = fx["gn"].astype(np.float64)
+    gns = np.stack([g, np.roll(g, 40, 0), g.T.copy()])
+    out = both(sgpmod.sgp_betaDiv_batch, gns, fx["psf"], 100.0, team=1, **kw)
+    assert int(out["iters"][0]) == int(fx["iters"])
+    r = np.linalg.norm(out["x"][0] - fx["x"]) / np.linalg.norm(fx["x"])
+    assert r < 1e-5, r
+    np.testing.assert_allclose(out["discr"][0, :int(fx["iters"]) + 1], fx["discr"], rtol=1e-7)
+
+
+def test_persistent_more_images_than_slots(sgpmod):
+    """1600 images (more than the workgroups the device holds at once): tasks
+    of iteration k + 1 wait for iteration k of the same image, handed over
+    between workgroups on other CUs and XCDs; bitwise the phase kernels."""
+    fx = golden("ref_lin64_beta.npz")
+    gn = fx["gn"].astype(np.float64)
+    rng = np.random.default_rng(11)
+    gns = np.stack([np.roll(np.roll(gn, int(rng.integers(64)), 0), int(rng.integers(64)), 1)
+                    for _ in range(1600)])
+    kw = dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=6, alpha=10.0,
+              ccd_sat_level=65000.0, use_original_SGP_Afunction=False, schedule_lr=True,
+              adapt_beta=False, betaParams=1.05, team=1)
+    both(sgpmod.sgp_betaDiv_batch, gns, fx["psf"], 100.0, **kw)

@@ -92,6 +92,24 @@ def test_oracle_linear_solves(name):
     np.testing.assert_allclose(discr, fx["discr"], rtol=1e-8)
 
 
+@pytest.mark.parametrize("name", ["c3long_s0", "c3stop3_s0"])
+def test_oracle_c3_long_trials(name):
+    """The timed workload to MAXIT 100 (and its stop-3 variant): the oracle
+    matches the reference's iterates and its line-search trials in every
+    iteration (tests/golden/make_golden.py long)."""
+    fx = golden(f"ref_{name}.npz")
+    kw = ref_kwargs(fx)
+    st = {}
+    x, it, discr, _, _ = orc.sgp_betaDiv(fx["gn"].astype(np.float64), fx["psf"], np.float64(100.0),
+                                         stats=st, **kw)
+    assert it == int(fx["iters"])
+    assert np.linalg.norm(x - fx["x"]) / np.linalg.norm(fx["x"]) < 1e-8
+    np.testing.assert_allclose(discr, fx["discr"], rtol=1e-8)
+    from conftest import compare_trials
+    diff = compare_trials(st["ls_trials"], fx["trials"], name)
+    print(name, "stagnating iterations with another trial count:", len(diff))
+
+
 # ------------------------------------------------- application drop-in path
 from conftest import APP_CASES, app_case  # noqa: E402
 

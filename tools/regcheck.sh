@@ -1,16 +1,16 @@
 #!/bin/bash
-# Print VGPR / spill / scratch of every kernel in bsgp_solver.hip (gfx950).
+# Print VGPR / spill / scratch of every kernel in a solver translation unit
+# (gfx950).  Usage: tools/regcheck.sh [file.hip (default bsgp_solver.hip)] [extra hipcc flags]
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
+SRC=${1:-bsgp_solver.hip}; shift || true
 D=$(mktemp -d)
 cd $D
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -mcode-object-version=5 \
-  -I $R/include -c $R/beta-sgp_amd/csrc/bsgp_solver.hip -o s.o -save-temps "$@" 2>/dev/null
-python3 - <<'PY'
-import re
-s=open('bsgp_solver-hip-amdgcn-amd-amdhsa-gfx950.s').read()
-for m in re.finditer(r'\.name:\s+(\S+)\n(.*?)(?=\n  - \.|\Z)', s, re.S):
-    pass
+  -I $R/include -c $R/beta-sgp_amd/csrc/$SRC -o s.o -save-temps "$@" 2>/dev/null
+python3 - "${SRC%.hip}" <<'PY'
+import re, sys
+s=open(f'{sys.argv[1]}-hip-amdgcn-amd-amdhsa-gfx950.s').read()
 blocks=s.split('.name:')
 for b in blocks[1:]:
     name=b.split()[0]
