@@ -83,7 +83,52 @@ CONFIGS = {
     "c5": dict(n=256, k=25, nstars=200, total=8192, circular=False,
                desc="{T} independent {n}x{n} subdivisions split over the GPUs ({B} on this "
                     "rank), 25x25 PSF, linear A"),
+    # application_sgp_star_stamps.py:56-105: 31x31 float32 cutouts around stars,
+    # the DIAPL PSF with the default circular A, adaptive beta, stop rule 3, the
+    # five seeds; the reference's only first-party throughput figure
+    "stamps31": dict(n=31, k=31, nstars=0, batch=16384, circular=True, stamps=True, maxit=500,
+                     desc="{B} float32 31x31 star stamps (cutouts of results/SUBDIV_ORIGIMG.fits "
+                          "at bright pixels) x the application's 5 seeds, DIAPL 31x31 PSF, "
+                          "circular A"),
 }
+STAMP_PUBLISHED = 1167.5  # it/s, beta-SGP star stamps (results/EXEC_TIME_BETA.npy, NUM_ITERS_BETA.npy)
+
+
+def stamp_inputs(B, seed=0):
+    """B star-stamp solves as application_sgp_star_stamps.py:56-105 makes
+    them: 31x31 float32 cutouts (Cutout2D at integer centres = slices) of the
+    reference's float32 frame results/SUBDIV_ORIGIMG.fits around bright
+    pixels (the brightest 2 % of the frame, drawn with replacement), each with
+    its float64 median as background and sum(cutout - bkg) as flux (stand-ins
+    for photutils' background_median and segment_flux), cycling through the
+    application's five seeds; the 31x31 DIAPL PSF.  Returns host arrays."""
+    import fits_io
+    gold = os.path.join(ROOT, "tests", "golden")
+    _, img = fits_io.read_fits(os.path.join(gold, "SUBDIV_ORIGIMG.fits"))
+    _, psf = fits_io.read_fits(os.path.join(gold, "psfccfbrd210048_1_1_img.fits"))
+    a = np.asarray(img, dtype=np.float32)
+    inner = a[15:-15, 15:-15]
+    thr = np.quantile(inner, 0.98)
+    rows, cols = np.nonzero(inner >= thr)
+    rng = np.random.default_rng(seed)
+    pick = rng.integers(0, len(rows), B)
+    cuts = np.stack([a[r:r + 31, c:c + 31] for r, c in zip(rows[pick], cols[pick])])
+    bkg = np.median(cuts.reshape(B, -1).astype(np.float64), axis=1)
+    flux = np.sum(cuts.astype(np.float64) - bkg[:, None, None], axis=(1, 2))
+    seeds = (0, 42, 951, 93, 810)  # application_sgp_star_stamps.py:69-75
+    betas = []
+    for s_ in seeds:
+        np.random.seed(s_)
+        betas.append(np.random.normal(loc=1, scale=0.05))
+    return cuts, np.asarray(psf, dtype=np.float64), bkg, flux, np.resize(np.asarray(betas), B)
+
+
+def stamp_kwargs(maxit):
+    """application_sgp_star_stamps.py:82-90 (DEFAULT_PARAMS unpacked, sgp.py:34)."""
+    return dict(gamma=1e-4, beta=0.4, alpha_min=1e-5, alpha_max=1e5, alpha=10.0, M_alpha=3,
+                tau=0.5, M=1, proj_type=1, max_projs=1000, init_recon=2, stop_criterion=3,
+                MAXIT=maxit, ccd_sat_level=65000, scale_data=True, lr=1e-3, lr_exp_param=0.1,
+                schedule_lr=True, adapt_beta=True, use_original_SGP_Afunction=True)
 
 
 def synth_batch(B, n, k, nstars, seed0, bkg=100.0, circular=False):
@@ -151,6 +196,24 @@ def cpu_baseline(n, k, nstars, images, maxit, workers, circular=False):
                       f"with oracle/sgp_oracle.py, one image per process on {workers} processes "
                       f"({cpu_model()}; the host shows {ncpu} CPUs, a one-GPU share is "
                       f"{CPU_CAP}): {iters} image-iterations in {wall:.1f}s wall "
+                      f"({iters / cpu_s:.1f} image-it/s per core)"}
+
+
+def cpu_baseline_stamps(kw, images, workers):
+    """The oracle on `images` stamps of the same stamp workload, one stamp per
+    task on `workers` processes."""
+    import cpu_bench
+    cuts, psf, bk, fl, betas = stamp_inputs(images, seed=777)
+    okw = {k_: v for k_, v in kw.items() if k_ in stamp_kwargs(1)}
+    jobs = [(cuts[i], psf, float(bk[i]), float(fl[i]), float(betas[i]), okw)
+            for i in range(images)]
+    iters, wall, cpu_s = cpu_bench.run_pool_jobs(jobs, workers)
+    ncpu = os.cpu_count() or 1
+    return {"value": iters / wall, "unit": "image-iterations/s", "cores": workers,
+            "kind": "port", "cpu_model": cpu_model(), "host_cpus": ncpu,
+            "sample": f"{images} float32 31x31 stamps of the same workload (adaptive beta, "
+                      f"stop 3) with oracle/sgp_oracle.py, one stamp per process on {workers} "
+                      f"processes ({cpu_model()}): {iters} image-iterations in {wall:.1f}s wall "
                       f"({iters / cpu_s:.1f} image-it/s per core)"}
 
 
@@ -252,7 +315,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (c2/c3/c4)")
-    ap.add_argument("--maxit", type=int, default=100)
+    ap.add_argument("--maxit", type=int, default=None, help="default 100 (500 for stamps31)")
     ap.add_argument("--ls-spec", type=int, default=None)
     ap.add_argument("--streams", type=int, default=None)
     ap.add_argument("--team", type=int, default=None,
@@ -265,6 +328,8 @@ def parse_args(argv=None):
     ap.add_argument("--stop3", action="store_true",
                     help="stop rule 3 (tol 1e-5, the application's) instead of stop rule 1")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end solve (host inputs -> host outputs)")
     ap.add_argument("--no-profile", action="store_true",
                     help="skip the profiled solve (per-kernel roofline)")
     ap.add_argument("--cpu-images", type=int, default=16)
@@ -301,6 +366,9 @@ def main():
 
     cfg = CONFIGS[args.config]
     n, k, nstars, circ = cfg["n"], cfg["k"], cfg["nstars"], cfg["circular"]
+    stamps = cfg.get("stamps", False)
+    if args.maxit is None:
+        args.maxit = cfg.get("maxit", 100)
     strong = "total" in cfg
     if strong:
         lo, hi = shard_bounds(cfg["total"], world, rank)
@@ -311,6 +379,10 @@ def main():
     kw = solve_kwargs(args.maxit, args.ls_spec, args.streams, args.team, circular=circ,
                       proj_cache=args.proj_cache, storage=args.storage,
                       persistent=args.persistent, stop3=args.stop3)
+    if stamps:
+        kw = dict(stamp_kwargs(args.maxit), ls_spec=args.ls_spec, streams=args.streams,
+                  team=args.team, proj_cache=args.proj_cache, storage=args.storage,
+                  persistent=args.persistent)
 
     if args.stub:
         def step():
@@ -323,8 +395,17 @@ def main():
         torch.cuda.set_device(local)
         import _bsgp
         import sgp
-        gn, psf = synth_batch(B, n, k, nstars, seed0=seed0, circular=circ)
-        bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
+        if stamps:
+            cuts, psf, bk_h, fl_h, betas = stamp_inputs(B, seed=seed0)
+            gn = torch.from_numpy(cuts).cuda()  # float32: the reference's float32 arithmetic
+            bkg = torch.from_numpy(bk_h).cuda()
+            flux = torch.from_numpy(fl_h).cuda()
+            extra = dict(betaParams=betas, flux=flux)
+        else:
+            gn, psf = synth_batch(B, n, k, nstars, seed0=seed0, circular=circ)
+            bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
+            extra = {}
+        kw.update(extra)
         torch.cuda.synchronize()
 
         def step():
@@ -365,11 +446,17 @@ def main():
     if rank != 0:
         return
 
-    workload = (f"{args.config.upper()}: "
-                + cfg["desc"].format(n=n, B=B, T=cfg.get("total", B))
-                + f", beta-SGP (beta=1.05), proj_type=1, MAXIT={args.maxit}, stop_criterion=1")
+    if stamps:
+        workload = (f"STAMPS31: " + cfg["desc"].format(B=B) + f", adaptive beta-SGP, proj_type=1, "
+                    f"init_recon=2, MAXIT={args.maxit}, stop_criterion=3 (tol 1e-4)")
+    else:
+        workload = (f"{args.config.upper()}: "
+                    + cfg["desc"].format(n=n, B=B, T=cfg.get("total", B))
+                    + f", beta-SGP (beta=1.05), proj_type=1, MAXIT={args.maxit}, "
+                      f"stop_criterion={kw['stop_criterion']}")
     result = {
-        "metric": "SGP iterations/sec (fp64) on batched 256x256 images",
+        "metric": ("SGP iterations/sec (fp64) on batched 31x31 float32 star stamps" if stamps
+                   else "SGP iterations/sec (fp64) on batched 256x256 images"),
         "value": value,
         "unit": "image-iterations/s",
         "n_gpus": world,
@@ -378,9 +465,14 @@ def main():
         "ms_per_step": elapsed_max / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
-        "vs_baseline": None,
+        "vs_baseline": (value / STAMP_PUBLISHED) if stamps else None,
         "dtype": "f64" if args.storage == "f64" else "f32 storage, f64 arithmetic",
-        "data": "synthetic (SURVEY §8d generator: pareto point sources * 25x25 Gaussian PSF "
+        "data": ("the reference's float32 frame results/SUBDIV_ORIGIMG.fits cut into 31x31 "
+                 "stamps around its brightest pixels (tests/golden copy), its DIAPL PSF; "
+                 "vs_baseline = value / 1167.5 it/s, the reference's published star-stamp "
+                 "beta-SGP rate (results/EXEC_TIME_BETA.npy, NUM_ITERS_BETA.npy; hardware "
+                 "unstated)") if stamps else
+                "synthetic (SURVEY §8d generator: pareto point sources * 25x25 Gaussian PSF "
                 "+ Poisson, bkg 100), built on device",
         "config": {"workload": workload, "images_per_gpu": B,
                    "images_total": cfg.get("total", B * world), "image": [n, n], "psf": [k, k],
@@ -409,13 +501,39 @@ def main():
                              "stop_criterion": kw["stop_criterion"]})
     if not args.no_profile:
         result["roofline"] = roofline(args, kw, gn, psf, bkg, B, n, kern_ms)
+    if not args.no_e2e:
+        result["end_to_end"] = end_to_end(kw, gn, psf, bkg)
     if world == 1 and not args.no_cpu:
         workers = max(1, min(CPU_CAP, os.cpu_count() or 1))
         images = args.cpu_images if B > 1 else 1
         cpu_maxit = args.cpu_maxit if args.cpu_maxit else args.maxit
-        result["cpu_baseline"] = cpu_baseline(n, k, nstars, images, cpu_maxit,
-                                              min(workers, images), circular=circ)
+        if stamps:
+            result["cpu_baseline"] = cpu_baseline_stamps(kw, args.cpu_images * 8,
+                                                         min(workers, args.cpu_images * 8))
+        else:
+            result["cpu_baseline"] = cpu_baseline(n, k, nstars, images, cpu_maxit,
+                                                  min(workers, images), circular=circ)
     print(json.dumps(result), flush=True)
+
+
+def end_to_end(kw, gn, psf, bkg):
+    """SURVEY §8d's second figure: one solve from host buffers to host buffers
+    (the drop-in's own path: the images and backgrounds copied to the device,
+    the solve, x / iters / discr / times / counters copied back), outside the
+    timed loop.  `value` is never this: it times the solve on resident data."""
+    import sgp
+    g_host = gn.cpu().numpy()
+    b_host = bkg.cpu().numpy()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = sgp.sgp_betaDiv_batch(g_host, psf, b_host, **kw)
+    el = time.perf_counter() - t0
+    its = float(np.sum(out["iters"]))
+    h2d = g_host.nbytes + b_host.nbytes
+    d2h = sum(v.nbytes for v in out.values() if isinstance(v, np.ndarray))
+    return {"value": its / el, "unit": "image-iterations/s", "ms": el * 1e3,
+            "h2d_bytes": int(h2d), "d2h_bytes": int(d2h),
+            "note": "host float64 arrays in, host arrays out (PCIe both ways), one solve"}
 
 
 def profile_kernels(kw, gn, psf, bkg, n):
@@ -430,7 +548,8 @@ def profile_kernels(kw, gn, psf, bkg, n):
                           else _bsgp.BSGP_CONV_LINEAR_FILL, storage=kw["storage"])
     cnt, iters = prof["counters"], prof["iters"]
     team = int(cnt[0, 5])
-    kb = kernel_bytes(n, n, plan.P, plan.Q // 2 + 1, cnt, iters, beta=True, series=True,
+    kb = kernel_bytes(n, n, plan.P, plan.Q // 2 + 1, cnt, iters, beta=True,
+                      series=not kw.get("adapt_beta", False),
                       compact=sgp.GN_COMPACT_DEFAULT == 1, bmap=False,
                       fused_at_col=(team == 1), vb=4.0 if kw["storage"] == "f32" else 8.0)
     kb["k_persist"] = float(sum(kb.values()))

@@ -254,7 +254,7 @@ static int ensure_team(bsgp_plan p, size_t B, int T) {
     HIP_TRY(hipMalloc(&p->tpart, np * sizeof(double)));
     p->tpart_n = np;
   }
-  const size_t cb = round_up((B + 1) * sizeof(unsigned int), 16);
+  const size_t cb = round_up((B * kTeamWords + kTeamLine) * sizeof(unsigned int), 128);
   if (cb > p->tctr_bytes) {
     if (p->tctr) HIP_TRY(hipFree(p->tctr));
     p->tctr = nullptr;
@@ -720,7 +720,7 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   a.fuse_col = T == 1 ? BSGP_FUSE_COL : 0;
   a.tpart = T > 1 ? p->tpart : nullptr;
   a.tctr = p->tctr;
-  a.tfail = reinterpret_cast<int*>(p->tctr + B);
+  a.tfail = reinterpret_cast<int*>(p->tctr + (size_t)B * kTeamWords);
   a.plist = nullptr;
   a.plist_stride = 0;
   a.lcap = 0;

@@ -202,13 +202,20 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned int gu32;
 typedef __attribute__((address_space(1))) int gi32;
 
+// Barrier words of one image (kTeamWords unsigned ints, every word on a
+// 128-B line of its own): per group g < 8 an arrival counter and a
+// generation word, and one top counter of completed groups.
+constexpr int kTeamLine = 32;
+constexpr int kTeamWords = 17 * kTeamLine;
+
 struct Team {
   int m, T;            // member index, team size
   double* part;        // [2][T][kMaxRed] partial slots of this image (double-buffered)
-  unsigned int* ctr;   // arrival counter of this image (monotonic across kernels)
-  unsigned int base;   // counter value when this kernel started (same in all members)
+  unsigned int* ctr;   // the image's kTeamWords barrier words (monotonic across kernels)
+  unsigned int base;   // barriers the team completed before this kernel (same in all members)
   int nb;              // team barriers passed in this kernel
   int* fail;           // set when a barrier spin times out (solve status bit 4)
+  int grp, ng, G;      // this member's group (blockIdx % 8), members in it, groups in the team
 };
 
 // Work partition of a team.  Waves: row pairs / columns strided by gws from
@@ -245,24 +252,45 @@ __device__ __forceinline__ Part solo_part(int nfw) {
   return d;
 }
 
-// Lane 0: arrive, then wait for all T members (bounded spin with s_sleep;
-// once any barrier of the solve timed out, later ones return at once and the
-// solve ends with status bit 4 instead of hanging).
+// Lane 0: arrive, then wait for all T members.  XCD-hierarchical
+// (MI355X_MICROARCH.md, barrier-xcd): members are grouped by blockIdx % 8 --
+// with the runtime's round-robin dispatch, the members on one XCD -- and each
+// arrives on its group's counter; the last arriver of a group (told by the
+// value its add returns) adds to the team's top counter, waits for all G
+// groups there and publishes the barrier's generation to its group, whose
+// other members poll only that word.  One top counter sees G <= 8 adds
+// instead of T, and no line is polled by more than a group.  The grouping
+// is only a speed choice: any placement gives the same barrier.  Bounded
+// spins with s_sleep; once any barrier of the solve timed out, later ones
+// return at once and the solve ends with status bit 4 instead of hanging.
+__device__ __forceinline__ bool team_spin(Team& t, unsigned& spins) {
+  __builtin_amdgcn_s_sleep(1);
+  ++spins;
+  if ((spins & 1023u) == 0 &&
+      __hip_atomic_load((gi32*)t.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+    return false;
+  if (spins > (1u << 24)) {
+    __hip_atomic_store((gi32*)t.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+  }
+  return true;
+}
 __device__ __forceinline__ void team_arrive_wait(Team& t) {
-  __hip_atomic_fetch_add((gu32*)t.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned int target = t.base + (unsigned int)(t.nb + 1) * (unsigned int)t.T;
+  const unsigned int n1 = t.base + (unsigned int)t.nb + 1;  // barriers done after this one
+  gu32* gc = (gu32*)(t.ctr + t.grp * kTeamLine);
+  gu32* gen = (gu32*)(t.ctr + (8 + t.grp) * kTeamLine);
+  gu32* top = (gu32*)(t.ctr + 16 * kTeamLine);
+  const unsigned int old = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned int spins = 0;
-  while ((int)(__hip_atomic_load((gu32*)t.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
-               target) < 0) {
-    __builtin_amdgcn_s_sleep(1);
-    ++spins;
-    if ((spins & 1023u) == 0 &&
-        __hip_atomic_load((gi32*)t.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
-      break;
-    if (spins > (1u << 24)) {
-      __hip_atomic_store((gi32*)t.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
+  if (old + 1 == n1 * (unsigned int)t.ng) {  // the group's last arrival
+    __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int target = n1 * (unsigned int)t.G;
+    while ((int)(__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0)
+      if (!team_spin(t, spins)) return;
+    __hip_atomic_store(gen, n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    while ((int)(__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - n1) < 0)
+      if (!team_spin(t, spins)) return;
   }
 }
 
@@ -1396,6 +1424,32 @@ __device__ __forceinline__ double beta_deriv_px(double y, double x, double b) {
   t = t - xb / (b * ((b - 1) * (b - 1)));
   t = t + yb * ly / b;
   t = t - xb / ((b * b) * (b - 1));
+  t = t - yb / (b * b);
+  return t;
+}
+
+// The same for a float32 observed image (params.gn_f32), as numpy 1.x
+// evaluates sgp.py:495 with x = gn float32 and y = den float64: the terms in
+// x**beta are float32 arrays (x**beta and np.log(x) in float32, their
+// product and the divisions by the float64 scalars, cast to float32, rounded
+// to float32), the others float64; the seven terms are added left to right,
+// each float32 term widened as it is added.
+__device__ __forceinline__ double beta_deriv_px_f32(double y, double x, double b) {
+  const double ly = fast_log(y);
+  const double yb1 = fast_exp((b - 1) * ly);
+  const double yb = fast_exp(b * ly);
+  const float xf = (float)x;
+  const float xb = (float)pow((double)xf, (double)(float)b);  // x**beta (float32)
+  const float lx = (float)log((double)xf);                      // np.log(x) (float32)
+  const float c3 = (float)(b * (b - 1));
+  const float c4 = (float)(b * ((b - 1) * (b - 1)));
+  const float c6 = (float)((b * b) * (b - 1));
+  double t = -x * yb1 * ly / (b - 1);
+  t = t + x * yb1 / ((b - 1) * (b - 1));
+  t = t + (double)((xb * lx) / c3);
+  t = t - (double)(xb / c4);
+  t = t + yb * ly / b;
+  t = t - (double)(xb / c6);
   t = t - yb / (b * b);
   return t;
 }

@@ -14,7 +14,7 @@ namespace bsgp {
 // Per-image solver state carried between the phase kernels (device memory).
 struct ImgState {
   int par, Xones, stop, iter, epoch;
-  int bar_base;  // team-barrier counter value at the start of the next kernel (T > 1)
+  int bar_base;  // team barriers completed before the next kernel (T > 1)
   int64_t E_p, E_ls, ls_passes, status, ls_series;
   int64_t proj_passes, proj_list;  // projection passes over the image / list entries read
   double sc, flux, bks_scalar, lo, hi, Dcoeff, tol, t0;
@@ -66,7 +66,7 @@ struct SolveArgs {
   int Tc;               // workgroups per image of k_col (no reductions there: not a team)
   int fuse_col;         // T == 1: BSGP_FUSE_COL (which phase kernels run the column passes)
   double* tpart;        // [B][2][T][kMaxRed] reduction partials
-  unsigned int* tctr;   // [B] barrier arrival counters, zeroed per solve
+  unsigned int* tctr;   // [B][kTeamWords] barrier words, then the timeout word; zeroed per solve
   int* tfail;           // set by a timed-out barrier spin
   // projection pixel lists (proj_cache): per image two arrays (y, X) of
   // lcap * T * kBlock doubles; entry k of global thread gt at k*T*kBlock + gt

@@ -294,21 +294,27 @@ __device__ __forceinline__ Team make_team(const SolveArgs& A, int img, const Img
   t.T = A.T;
   t.m = A.T == 1 ? 0 : (int)(blockIdx.x % (unsigned)A.T);
   t.part = A.tpart ? A.tpart + (size_t)img * 2 * A.T * kMaxRed : nullptr;
-  t.ctr = A.tctr ? A.tctr + img : nullptr;
+  t.ctr = A.tctr ? A.tctr + (size_t)img * kTeamWords : nullptr;
   t.base = (unsigned int)st.bar_base;
   t.nb = 0;
   t.fail = A.tfail;
+  // barrier groups: blockIdx % 8 (the XCD under round-robin dispatch)
+  t.grp = (int)(blockIdx.x & 7u);
+  const unsigned first = blockIdx.x - (unsigned)t.m;  // the team's first workgroup
+  const int r = (int)(((unsigned)t.grp - (first & 7u)) & 7u);
+  t.ng = t.T / 8 + (r < (t.T & 7) ? 1 : 0);
+  t.G = t.T < 8 ? t.T : 8;
   return t;
 }
 __device__ __forceinline__ int team_img(const SolveArgs& A) {
   return A.img0 + (A.T == 1 ? (int)blockIdx.x : (int)(blockIdx.x / (unsigned)A.T));
 }
-// Member 0 records where the barrier counter stands for the next kernel; all
-// members read bar_base before their first arrival, member 0 writes it after
-// its last one, so no member can see the new value early.
+// Member 0 records how many team barriers the image has completed, for the
+// next kernel; all members read bar_base before their first arrival, member
+// 0 writes it after its last one, so no member can see the new value early.
 __device__ __forceinline__ void team_end(ImgState& st, const Team& t) {
   if (t.T > 1 && t.m == 0 && threadIdx.x == 0 && t.nb > 0)
-    st.bar_base = (int)(t.base + (unsigned int)t.T * (unsigned int)t.nb);
+    st.bar_base = (int)(t.base + (unsigned int)t.nb);
 }
 __device__ __forceinline__ bool leader(const Team& t) { return t.m == 0 && threadIdx.x == 0; }
 
@@ -584,7 +590,7 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     st.stop = 0;
     st.iter = 1;
     st.epoch = 0;
-    st.bar_base = (int)((unsigned int)tm.T * (unsigned int)tm.nb);
+    st.bar_base = tm.nb;
     st.E_p = st.E_ls = st.ls_passes = st.status = st.ls_series = 0;
     st.proj_passes = st.proj_list = 0;
     st.lam_p = 0.0;  // no previous multiplier: the first projection splits no bracket
@@ -985,6 +991,26 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
   // The lambda-independent sum (sum s*gn^b, or sum gn at beta = 1) is carried
   // in the state; with adaptive beta it changes with beta and is recomputed.
   double konst = st.konst;
+  // Adaptive beta on a float32 image (params.gn_f32): the reference re-sums
+  // s*gn**beta at every trial's beta as float32 terms in numpy's float32
+  // order (sgp.py:458, 782), and the float32 terms of betaDivDeriv round to
+  // float32 (beta_deriv_px_f32).  pw is free scratch until the accept
+  // rewrites it (no series moments with adaptive beta).
+  const bool k32 = ADAPT && P.gn_f32 != 0;
+  auto konst32 = [&](double b) -> double {
+    const float sf = (float)(1 / (b * (b - 1)));
+    const double bf = (double)(float)b;  // x**beta: the exponent is cast to float32
+    return (double)np_f32_sum(
+        A.pw,
+        [&](int i) {
+          const double g = g32 ? gdec1(reinterpret_cast<const float*>(B.gns)[i]) : B.gns[i];
+          return sf * (float)pow(g, bf);
+        },
+        reinterpret_cast<float*>(B.pw), Pt, tm);
+  };
+  auto bderiv = [&](double den, double g, double b) __attribute__((always_inline)) {
+    return k32 ? beta_deriv_px_f32(den, g, b) : beta_deriv_px(den, g, b);
+  };
   // Small-step series (general beta, fixed beta): with den_i(lam) =
   // a_i (1 + lam u_i), a_i = x_tf_i + bkg_i, u_i = d_tf_i / a_i,
   //   sum den^b        = sum_m binom(b, m)   lam^m P_m,  P_m = sum a^b u^m
@@ -1029,8 +1055,8 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
       const double xt = x0 + lam * v;
       obj.template terms_m<MODE>(xt, xt + bkv, g, &t1[0]);
       if constexpr (adapt) {
-        t1[2] += obj.konst(g);
-        t1[3] += beta_deriv_px(xt + bkv, g, obj.beta);
+        if (!k32) t1[2] += obj.konst(g);
+        t1[3] += bderiv(xt + bkv, g, obj.beta);
       }
       if (series) {
         const double a = x0 + bkv;
@@ -1063,7 +1089,7 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
         ser[MS + 1 + m] = t1[4 + MS + 1 + m];
       }
     }
-    if (adapt) konst = t1[2];
+    if (adapt) konst = k32 ? konst32(obj.beta) : t1[2];
     ++passes;
     ++nls;
     const double f1 = obj.combine(konst, t1[0], t1[1], flux, (double)N);
@@ -1127,7 +1153,9 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
 #pragma unroll
     for (int k = 0; k < NT; ++k) t[k] = 0.0;
     auto eval_px = [&](double x0, double dt, double g, double bkv) __attribute__((always_inline)) {
-      if constexpr (adapt) t[2 * K] += obj.konst(g);
+      if constexpr (adapt) {
+        if (!k32) t[2 * K] += obj.konst(g);
+      }
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const double xt = x0 + lamk[k] * dt;
@@ -1135,7 +1163,7 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
         obj.template terms_m<MODE>(xt, den, g, &t[2 * k]);
       }
       if constexpr (K == 1 && adapt)
-        t[2 * K + 1] += beta_deriv_px(x0 + lamk[0] * dt + bkv, g, obj.beta);
+        t[2 * K + 1] += bderiv(x0 + lamk[0] * dt + bkv, g, obj.beta);
     };
     const V* xtf = B.xtf;
     const V* dtf = B.dtf;
@@ -1164,7 +1192,7 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
           if (!odd || 2 * p + 1 < N) eval_px(v.x.y, v.d.y, g1, v.b.y);
         });
     team_sum<NT>(t, red, tm);
-    if (adapt) konst = t[2 * K];
+    if (adapt) konst = k32 ? konst32(obj.beta) : t[2 * K];
     ++passes;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -1462,33 +1490,47 @@ __device__ __forceinline__ unsigned ld_sc1_u32(const unsigned* p) {
 }
 
 // The phases of a task are separate (noinline) functions, so each keeps the
-// register allocation of its own kernel; their argument block is re-read from
-// the kernarg segment (scalar loads) through a pointer the compiler cannot see
-// through.  Inlined into one kernel body the phases spilled 57-88 VGPRs inside
-// their loops at the 168 VGPRs of 3 waves/SIMD (the scalar state of all
-// phases at once); as calls the only spill code is each phase's callee-saved
-// registers at its entry and exit (~210 VGPRs per wave per task, ~3 % of a
-// task's bytes, L2-resident).
+// register allocation of its own kernel.  Their argument block is the
+// kernel's own (the kernarg segment): the kernel passes its address, the
+// callee makes it wave-uniform (readfirstlane) and reads it as constant
+// memory, i.e. with scalar loads (the kernarg-segment intrinsic itself
+// yields 0 outside a kernel).  Inlined into one kernel body the phases
+// spilled 57-88 VGPRs inside their loops at the 168 VGPRs of 3 waves/SIMD (the
+// scalar state of all phases at once); as calls the only spill code is each
+// phase's callee-saved registers at its entry and exit (~210 VGPRs per wave
+// per task, ~3 % of a task's bytes, L2-resident).
 #ifndef BSGP_PERSIST_CALLS
 #define BSGP_PERSIST_CALLS 1
 #endif
-__device__ __forceinline__ const SolveArgs& kernarg_args() {
-  typedef const __attribute__((address_space(4))) SolveArgs* KP;
-  KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(p));
-  return *(const SolveArgs*)p;
-}
 #if BSGP_PERSIST_CALLS
 #define BSGP_PERSIST_FN __attribute__((noinline))
 #else
 #define BSGP_PERSIST_FN __forceinline__
 #endif
-template <class V>
-__device__ BSGP_PERSIST_FN void persist_dir(int img) {
-  dir_phase<false, V>(kernarg_args(), img);
+struct ArgRef {
+  unsigned lo, hi;  // address of the kernel's SolveArgs (kernarg segment)
+};
+__device__ __forceinline__ ArgRef kernarg_ref() {
+  const unsigned long long a = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
+  return ArgRef{(unsigned)a, (unsigned)(a >> 32)};
 }
-__device__ BSGP_PERSIST_FN void persist_col_a(int img) {
-  const SolveArgs& A = kernarg_args();
+__device__ __forceinline__ const SolveArgs& args_of(ArgRef r) {
+  typedef const __attribute__((address_space(4))) SolveArgs* KP;
+  // (readfirstlane returns int: widen through unsigned, no sign extension)
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)r.lo);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)r.hi);
+  const unsigned long long a = ((unsigned long long)hi << 32) | (unsigned long long)lo;
+  KP p = (KP)a;
+  asm volatile("" : "+s"(p));  // re-read per call: nothing of it is hoisted across phases
+  return *(const SolveArgs*)p;
+}
+template <class V>
+__device__ BSGP_PERSIST_FN void persist_dir(ArgRef r, int img) {
+  dir_phase<false, V>(args_of(r), __builtin_amdgcn_readfirstlane(img));
+}
+__device__ BSGP_PERSIST_FN void persist_col_a(ArgRef r, int img) {
+  const SolveArgs& A = args_of(r);
+  img = __builtin_amdgcn_readfirstlane(img);
   BSGP_LDS_VIEWS(A);
   (void)red;
   Team tm{};
@@ -1499,12 +1541,12 @@ __device__ BSGP_PERSIST_FN void persist_col_a(int img) {
   PH_ADD(3, tc0);
 }
 template <int K, int MODE, bool ADAPT, class V>
-__device__ BSGP_PERSIST_FN void persist_ls(int img) {
-  ls_phase<K, MODE, ADAPT, false, V>(kernarg_args(), img);
+__device__ BSGP_PERSIST_FN void persist_ls(ArgRef r, int img) {
+  ls_phase<K, MODE, ADAPT, false, V>(args_of(r), __builtin_amdgcn_readfirstlane(img));
 }
 template <class V>
-__device__ BSGP_PERSIST_FN void persist_bb(int img) {
-  bb_phase<false, V>(kernarg_args(), img);
+__device__ BSGP_PERSIST_FN void persist_bb(ArgRef r, int img) {
+  bb_phase<false, V>(args_of(r), __builtin_amdgcn_readfirstlane(img));
 }
 
 template <int K, int MODE, bool ADAPT, class V>
@@ -1560,12 +1602,13 @@ __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs 
     if (t >= total) break;
     if (skip) continue;
     const int img = A.img0 + (int)(t % nimg);
-    persist_dir<V>(img);
+    const ArgRef ar = kernarg_ref();
+    persist_dir<V>(ar, img);
     __syncthreads();  // rows of d and the direction scalars complete
-    persist_col_a(img);
-    persist_ls<K, MODE, ADAPT, V>(img);
+    persist_col_a(ar, img);
+    persist_ls<K, MODE, ADAPT, V>(ar, img);
     __syncthreads();  // the accepted step and AT's columns complete
-    persist_bb<V>(img);
+    persist_bb<V>(ar, img);
     // publish iteration k of img: every wave's stores drained, then lane 0
     // releases at agent scope and stores the flag (sc1)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

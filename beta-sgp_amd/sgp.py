@@ -73,7 +73,7 @@ STREAMS_DEFAULT = 8 if _hw_queues() >= 8 else 4
 TEAM_DEFAULT = 0  # workgroups per image: 0 = auto (spread small batches over the CUs)
 PROJ_CACHE_DEFAULT = 1  # projectDF evaluations inside a known root bracket read a pixel list
 GN_COMPACT_DEFAULT = 1  # f32-exact observed images stored in f32 (bit-identical results)
-PERSIST_DEFAULT = 0  # one-workgroup batches: all iterations in one persistent launch
+PERSIST_DEFAULT = 1  # one-workgroup batches: all iterations in one persistent launch (C3 +1.4 %, A/B)
 
 
 # ------------------------------------------------------------------ helpers

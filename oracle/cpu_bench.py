@@ -71,3 +71,27 @@ def run_pool(n, k, nstars, images, kw, workers):
                        chunksize=1)
         wall = time.perf_counter() - t0
     return sum(r[0] for r in res), wall, sum(r[1] for r in res)
+
+
+def solve_job(args):
+    """One star-stamp solve with the oracle (bench.py stamps31): (cutout,
+    psf, bkg, flux, beta, kwargs) -> (iters, seconds)."""
+    cut, psf, bkg, flux, beta, kw = args
+    import sgp_oracle
+    t = time.perf_counter()
+    _, it, _, _, _ = sgp_oracle.sgp_betaDiv(cut, psf, np.float64(bkg), flux=np.float64(flux),
+                                            betaParam=beta, **kw)
+    return it, time.perf_counter() - t
+
+
+def run_pool_jobs(jobs, workers):
+    import multiprocessing as mp
+    os.environ["OMP_NUM_THREADS"] = "1"
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(workers) as pool:
+        pool.map(warm, range(workers))
+        t0 = time.perf_counter()
+        res = pool.map(solve_job, jobs, chunksize=1)
+        wall = time.perf_counter() - t0
+    return sum(r[0] for r in res), wall, sum(r[1] for r in res)

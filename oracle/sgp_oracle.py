@@ -97,7 +97,12 @@ def make_operators(psf, shape, circular):
 
 # ------------------------------------------------------------ beta-divergence
 def betaDiv(y, x, betaParam):
-    """sgp.py:441-458."""
+    """sgp.py:441-458.  betaParam enters as a Python float: numpy 1.x (the
+    reference's) casts a float64 SCALAR to a float32 array's dtype (value-based
+    casting), as numpy 2 does for a Python float -- after an adaptive update
+    (sgp.py:800) the reference's betaParam is a numpy float64, and the
+    float32 terms of a float32 image (x ** betaParam) must stay float32."""
+    betaParam = float(betaParam)
     if betaParam == 0:
         return np.sum(x / y) - np.sum(np.log(x / y)) - x.size
     elif betaParam == 1:
@@ -111,7 +116,7 @@ def betaDivDeriv(y, x, betaParam):
     """sgp.py:462-495 (d betaDiv / d beta, elementwise)."""
     if betaParam == 0 or betaParam == 1:
         return 0
-    b = betaParam
+    b = float(betaParam)  # numpy 1.x scalar casting (see betaDiv)
     return (-x * y ** (b - 1) * np.log(y) / (b - 1) + x * y ** (b - 1) / (b - 1) ** 2
             + x ** b * np.log(x) / (b * (b - 1)) - x ** b / (b * (b - 1) ** 2)
             + y ** b * np.log(y) / b - x ** b / (b ** 2 * (b - 1)) - y ** b / b ** 2)

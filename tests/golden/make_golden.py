@@ -119,7 +119,7 @@ def run_quiet(fn, *a, **k):
         return fn(*a, **k)
 
 
-def run_counted(sgp, fn, *a, **k):
+def run_counted(sgp, fn, *a, stdout=None, **k):
     """run_quiet(getattr(sgp, fn), ...) that also returns the reference's
     line-search trials of every iteration: the calls of the module-level
     betaDiv (restoration/sgp.py:782) between two calls of the module-level
@@ -140,7 +140,10 @@ def run_counted(sgp, fn, *a, **k):
 
     sgp.betaDiv, sgp.projectDF = b, p
     try:
-        out = run_quiet(getattr(sgp, fn), *a, **k)
+        import contextlib
+        import io
+        with contextlib.redirect_stdout(io.StringIO() if stdout is None else stdout):
+            out = getattr(sgp, fn)(*a, **k)
     finally:
         sgp.betaDiv, sgp.projectDF = ob, op
     trials, cur = [], None
@@ -412,6 +415,68 @@ def make_long():
               f"discrN={discr[-1]:.12f}")
 
 
+def star_positions(img, n, half=15, sep=31):
+    """Bright local maxima of img whose (2*half+1)^2 cutout lies inside the
+    frame, at least sep pixels apart, brightest first: (x, y) = (col, row)."""
+    from scipy import ndimage
+    a = np.asarray(img, dtype=np.float64)
+    peak = (a == ndimage.maximum_filter(a, size=7))
+    rows, cols = np.nonzero(peak)
+    order = np.argsort(-a[rows, cols], kind="stable")
+    out = []
+    for k in order:
+        r, c = int(rows[k]), int(cols[k])
+        if not (half <= r < a.shape[0] - half and half <= c < a.shape[1] - half):
+            continue
+        if all(max(abs(r - rr), abs(c - cc)) >= sep for cc, rr in out):
+            out.append((c, r))
+        if len(out) == n:
+            break
+    return out
+
+
+def make_stamps():
+    """application_sgp_star_stamps.py:56-105: 31x31 Cutout2D stamps of a
+    float32 frame (results/SUBDIV_ORIGIMG.fits, >f4) around bright stars, the
+    31x31 DIAPL PSF (psf/psfccfbrd210048_1_1_img.fits) with the DEFAULT
+    circular A (use_original_SGP_Afunction=True), adapt_beta=True, stop rule 3
+    (tol_convergence default 1e-4), the five seeds, init_recon 2, projection.
+    photutils is absent: the background is the cutout's float64 median (for
+    orig_bkg.background_median) and the flux sum(cutout - bkg) (for the star's
+    segment_flux); the stars are the frame's brightest local maxima.  The
+    final betaParam of every run (printed by sgp.py:892) is recorded."""
+    import io
+    sgp, fcp = import_reference(need_astropy=True)
+    from astropy.io import fits
+    from astropy.nddata import Cutout2D
+    img = fits.getdata("/root/reference/results/SUBDIV_ORIGIMG.fits")  # (375, 375) >f4
+    psf = fits.getdata("/root/reference/psf/psfccfbrd210048_1_1_img.fits")  # (31, 31) >f8
+    pos = star_positions(img, 8)
+    out = {"pos": np.array(pos, dtype=np.int32), "betas": np.array(app_betas())}
+    for j, (x, y) in enumerate(pos):
+        cut = Cutout2D(img, (x, y), size=31).data
+        assert cut.shape == (31, 31) and cut.dtype == np.dtype(">f4")
+        bkg = np.float64(np.median(cut))
+        flux = np.float64(np.sum(cut - bkg))
+        out[f"bkg{j}"], out[f"flux{j}"], out[f"cut{j}"] = bkg, flux, cut
+        for i, b in enumerate(app_betas()):
+            kw = dict(gamma=1e-4, beta=0.4, alpha_min=1e-5, alpha_max=1e5, alpha=10.0, M_alpha=3,
+                      tau=0.5, M=1, proj_type=1, max_projs=1000, init_recon=2, stop_criterion=3,
+                      save=False, verbose=True, flux=flux, ccd_sat_level=65000, scale_data=True,
+                      betaParam=b, lr=1e-3, lr_exp_param=0.1, schedule_lr=True, adapt_beta=True)
+            buf = io.StringIO()
+            (x_, it, discr, _, _), trials = run_counted(sgp, "sgp_betaDiv", cut, psf, bkg,
+                                                        stdout=buf, **kw)
+            line = [l for l in buf.getvalue().splitlines() if "final value" in l][-1]
+            out[f"x{j}_{i}"], out[f"iters{j}_{i}"], out[f"discr{j}_{i}"] = x_, it, discr
+            out[f"trials{j}_{i}"] = trials
+            out[f"beta{j}_{i}"] = np.float64(line.split(":")[-1])
+        print(f"stamp {j} at {x, y}: iters", [int(out[f"iters{j}_{i}"]) for i in range(5)])
+    kws = {k: v for k, v in kw.items() if k not in ("flux", "betaParam")}
+    out["kwargs"] = repr(kws)
+    np.savez_compressed(os.path.join(OUT, "ref_stamps31.npz"), **out)
+
+
 def make_c4():
     """BASELINE config C4's field (2048x2048, 5000 stars, 64x64
     Gaussian PSF embedded at the centre, circular A, beta = 1.05, projection)
@@ -577,6 +642,8 @@ if __name__ == "__main__":
                 make_long()
             elif which == "c4":
                 make_c4()
+            elif which == "stamps":
+                make_stamps()
             else:
                 make_linear()
         finally:

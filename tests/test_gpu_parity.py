@@ -417,8 +417,13 @@ def test_profiled_solve_reports_every_kernel_class(sgpmod):
     b = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, team=1, profile=True, **kw)
     np.testing.assert_array_equal(a["x"], b["x"])
     it = int(kw["MAXIT"])
-    assert list(b["launches"]) == [1, it, it, it, it]  # setup, dir, col (A), ls (+AT), bb
-    assert np.all(b["kernel_ms"] > 0)
+    # setup, dir, col (A), ls (+AT), bb; no persistent launch
+    assert list(b["launches"]) == [1, it, it, it, it, 0]
+    assert np.all(b["kernel_ms"][:5] > 0)
+    c = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, team=1, profile=True, persistent=1, **kw)
+    np.testing.assert_array_equal(a["x"], c["x"])
+    assert list(c["launches"]) == [1, 0, 0, 0, 0, 1]  # setup, then every iteration in one launch
+    assert c["kernel_ms"][5] > 0
 
 
 # ------------------------------------------------------- float32 storage (C4)

@@ -92,22 +92,44 @@ def test_oracle_linear_solves(name):
     np.testing.assert_allclose(discr, fx["discr"], rtol=1e-8)
 
 
-@pytest.mark.parametrize("name", ["c3long_s0", "c3stop3_s0"])
-def test_oracle_c3_long_trials(name):
+@pytest.mark.parametrize("name,xtol,dtol", [("c3long_s0", 1e-8, 1e-8), ("c3long_s1", 1e-8, 1e-8),
+                                            ("c3long_s2", 1e-4, 1e-5), ("c3stop3_s0", 1e-8, 1e-8)])
+def test_oracle_c3_long_trials(name, xtol, dtol):
     """The timed workload to MAXIT 100 (and its stop-3 variant): the oracle
-    matches the reference's iterates and its line-search trials in every
-    iteration (tests/golden/make_golden.py long)."""
+    matches the reference's iterates, and its line-search trials wherever the
+    accepted step is above the objective's rounding floor
+    (tests/golden/make_golden.py long; conftest.compare_trials).  Seed 2's
+    reference trajectory is unstable around iteration 55: a faithful
+    restatement parts from it there by ~5e-5 (test_gpu_long.py TOL)."""
     fx = golden(f"ref_{name}.npz")
     kw = ref_kwargs(fx)
     st = {}
     x, it, discr, _, _ = orc.sgp_betaDiv(fx["gn"].astype(np.float64), fx["psf"], np.float64(100.0),
                                          stats=st, **kw)
     assert it == int(fx["iters"])
-    assert np.linalg.norm(x - fx["x"]) / np.linalg.norm(fx["x"]) < 1e-8
-    np.testing.assert_allclose(discr, fx["discr"], rtol=1e-8)
+    assert np.linalg.norm(x - fx["x"]) / np.linalg.norm(fx["x"]) < xtol
+    np.testing.assert_allclose(discr, fx["discr"], rtol=dtol)
     from conftest import compare_trials
     diff = compare_trials(st["ls_trials"], fx["trials"], name)
     print(name, "stagnating iterations with another trial count:", len(diff))
+
+
+def test_oracle_star_stamps_adaptive_float32():
+    """application_sgp_star_stamps.py's workload (make_golden.py stamps): 8
+    stars x the 5 seeds, float32 31x31 cutouts, circular A, adaptive beta,
+    stop rule 3.  The oracle keeps numpy 1.x's float32 terms (betaParam as a
+    weak scalar); see conftest.stamp_parity for the bar.  At most 3 of the 40
+    chaotic runs may part from the reference after an iteration whose trial
+    count differs."""
+    from conftest import stamp_case, stamp_parity
+    parted = 0
+    for j in range(8):
+        for i in range(5):
+            gn, psf, bkg, kw, ref = stamp_case(j, i)
+            st = {}
+            x, it, discr, _, _ = orc.sgp_betaDiv(gn, psf, bkg, stats=st, **kw)
+            parted += not stamp_parity(x, it, discr, st["ls_trials"], st["beta"], ref)[0]
+    assert parted <= 3, parted
 
 
 # ------------------------------------------------- application drop-in path
