@@ -96,6 +96,30 @@ def make_operators(psf, shape, circular):
 
 
 # ------------------------------------------------------------ beta-divergence
+# Test hook: when True, the float32 terms x**beta and log(x) of a float32 image
+# are the correctly rounded float32 values (computed in float64, rounded once),
+# the device's arithmetic (bsgp_device.hpp beta_deriv_px_f32, bsgp_kernels.hpp
+# konst32), instead of numpy's vectorised float32 power/log, whose results may
+# be 1 ulp off.  False (the default) is the reference's arithmetic.
+CR_F32 = False
+
+
+def _is_f32(x):
+    return isinstance(x, np.ndarray) and x.dtype.kind == "f" and x.dtype.itemsize == 4
+
+
+def _pow(x, b):
+    if CR_F32 and _is_f32(x):
+        return (x.astype(np.float64) ** float(np.float32(b))).astype(np.float32)
+    return x ** b
+
+
+def _log(x):
+    if CR_F32 and _is_f32(x):
+        return np.log(x.astype(np.float64)).astype(np.float32)
+    return np.log(x)
+
+
 def betaDiv(y, x, betaParam):
     """sgp.py:441-458.  betaParam enters as a Python float: numpy 1.x (the
     reference's) casts a float64 SCALAR to a float32 array's dtype (value-based
@@ -108,7 +132,7 @@ def betaDiv(y, x, betaParam):
     elif betaParam == 1:
         return np.sum(np.multiply(x, np.log(np.divide(x, y)))) - np.sum(x) + np.sum(y)
     scal = 1 / (betaParam * (betaParam - 1))
-    return (np.sum(scal * x ** betaParam) + np.sum(scal * (betaParam - 1) * y ** betaParam)
+    return (np.sum(scal * _pow(x, betaParam)) + np.sum(scal * (betaParam - 1) * y ** betaParam)
             - np.sum(scal * betaParam * x * y ** (betaParam - 1)))
 
 
@@ -117,9 +141,10 @@ def betaDivDeriv(y, x, betaParam):
     if betaParam == 0 or betaParam == 1:
         return 0
     b = float(betaParam)  # numpy 1.x scalar casting (see betaDiv)
+    xb = _pow(x, b)
     return (-x * y ** (b - 1) * np.log(y) / (b - 1) + x * y ** (b - 1) / (b - 1) ** 2
-            + x ** b * np.log(x) / (b * (b - 1)) - x ** b / (b * (b - 1) ** 2)
-            + y ** b * np.log(y) / b - x ** b / (b ** 2 * (b - 1)) - y ** b / b ** 2)
+            + xb * _log(x) / (b * (b - 1)) - xb / (b * (b - 1) ** 2)
+            + y ** b * np.log(y) / b - xb / (b ** 2 * (b - 1)) - y ** b / b ** 2)
 
 
 def betaDivDerivwrtY(AT, den_arg, gn_arg, betaParam):

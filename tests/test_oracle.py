@@ -132,6 +132,27 @@ def test_oracle_star_stamps_adaptive_float32():
     assert parted <= 3, parted
 
 
+def test_oracle_star_stamps_correctly_rounded_f32():
+    """The same 40 runs with correctly rounded float32 power and log
+    (sgp_oracle.CR_F32, the device's arithmetic; test_gpu_stamps.py pins the
+    device to this oracle): parts from the reference only where an ulp of
+    numpy's float32 power flips a late line-search test -- the discrepancy
+    agrees up to that iteration -- and in at most 12 runs."""
+    from conftest import konst_ulp_discr, stamp_case, stamp_oracle_cr, stamp_parity
+    parted = []
+    for j in range(8):
+        for i in range(5):
+            gn, _, _, _, ref = stamp_case(j, i)
+            cr = stamp_oracle_cr(j, i)
+            ok, r, k = stamp_parity(cr["x"], cr["iters"], cr["discr"], cr["trials"], cr["beta"],
+                                    ref, atol=konst_ulp_discr(gn, cr["beta"]))
+            if not ok:
+                assert k >= 15, (j, i, k)  # a late iteration: the runs' stagnating end
+                parted.append((j, i, k))
+    print("correctly rounded oracle parts from the reference in", parted)
+    assert len(parted) <= 12, parted
+
+
 # ------------------------------------------------- application drop-in path
 from conftest import APP_CASES, app_case  # noqa: E402
 

@@ -6,7 +6,7 @@ FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts
 64 B per 128-B request of a wide coalesced stream, i.e. exactly half of the
 bytes (MI355X_MICROARCH.md §HBM), so it is doubled; WRITE_SIZE is exact for
 16-B/lane stores.  Both count the L2's fabric requests (Infinity-Cache hits
-included).  For every solver kernel class (k_setup, k_dir, k_col, k_ls, k_bb)
+included).  For every solver kernel class (k_setup, k_dir, k_col, k_ls, k_bb, k_persist)
 the bytes are averaged over its dispatches, giving HBM bytes per launch to
 compare with bench.py's per-kernel algorithmic bytes (run the PMC passes with
 --streams 1 so a launch is the whole batch, as in bench.py's profiled solve).
@@ -16,7 +16,7 @@ import json
 import sys
 from collections import defaultdict
 
-SOLVER = ("k_setup", "k_dir", "k_col", "k_ls", "k_bb")
+SOLVER = ("k_setup", "k_dir", "k_col", "k_ls", "k_bb", "k_persist")
 
 
 def load(f, ctr):
