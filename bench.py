@@ -98,7 +98,8 @@ def stamp_inputs(B, seed=0):
     """B star-stamp solves as application_sgp_star_stamps.py:56-105 makes
     them: 31x31 float32 cutouts (Cutout2D at integer centres = slices) of the
     reference's float32 frame results/SUBDIV_ORIGIMG.fits around bright
-    pixels (the brightest 2 % of the frame, drawn with replacement), each with
+    pixels (the brightest 2 % of the frame, drawn with replacement; stamps
+    with flux <= 0 redrawn), each with
     its float64 median as background and sum(cutout - bkg) as flux (stand-ins
     for photutils' background_median and segment_flux), cycling through the
     application's five seeds; the 31x31 DIAPL PSF.  Returns host arrays."""
@@ -112,9 +113,21 @@ def stamp_inputs(B, seed=0):
     rows, cols = np.nonzero(inner >= thr)
     rng = np.random.default_rng(seed)
     pick = rng.integers(0, len(rows), B)
-    cuts = np.stack([a[r:r + 31, c:c + 31] for r, c in zip(rows[pick], cols[pick])])
-    bkg = np.median(cuts.reshape(B, -1).astype(np.float64), axis=1)
-    flux = np.sum(cuts.astype(np.float64) - bkg[:, None, None], axis=(1, 2))
+
+    def cut(p):
+        c = np.stack([a[r:r + 31, c_:c_ + 31] for r, c_ in zip(rows[p], cols[p])])
+        b = np.median(c.reshape(len(p), -1).astype(np.float64), axis=1)
+        return c, b, np.sum(c.astype(np.float64) - b[:, None, None], axis=(1, 2))
+
+    cuts, bkg, flux = cut(pick)
+    # a source's segment flux is positive; a bright pixel inside a stamp whose
+    # median exceeds its mean (a hot pixel on a dip) is no star: redrawn, as
+    # the reference raises on it (no positive entry in flux/(flux+bkg)*AT(gn))
+    bad = np.nonzero(flux <= 0)[0]
+    while bad.size:
+        pick[bad] = rng.integers(0, len(rows), bad.size)
+        cuts[bad], bkg[bad], flux[bad] = cut(pick[bad])
+        bad = bad[flux[bad] <= 0]
     seeds = (0, 42, 951, 93, 810)  # application_sgp_star_stamps.py:69-75
     betas = []
     for s_ in seeds:

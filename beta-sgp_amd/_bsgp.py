@@ -265,6 +265,7 @@ class Plan:
 
 STATUS_LS_CAP = 1
 STATUS_TEAM_TIMEOUT = 4
+STATUS_NO_POSITIVE_BOUND = 8
 
 
 def check_status(counters):
@@ -272,9 +273,17 @@ def check_status(counters):
     are not valid.  Bit 1: the line search hit its trial cap, which happens
     only for a backtracking factor outside (0, 1), where the reference's
     loop (sgp.py:328-349 / 776-801) never terminates; bit 4: a team barrier
-    timed out (workgroups not co-resident)."""
+    timed out (workgroups not co-resident); bit 8: y = flux/(flux+bkg)*AT(gn)
+    has no positive entry, where the reference raises numpy's ValueError
+    (np.min of an empty array, sgp.py:269-270 / 711-712) -- raised here as
+    ValueError too."""
     c = counters.cpu().numpy() if hasattr(counters, "cpu") else np.asarray(counters)
     st = c[:, 3]
+    if np.any(st & STATUS_NO_POSITIVE_BOUND):
+        bad = np.nonzero(st & STATUS_NO_POSITIVE_BOUND)[0].tolist()
+        raise ValueError("zero-size array to reduction operation minimum which has no identity "
+                         f"(image(s) {bad[:8]}: y = flux/(flux+bkg)*AT(gn) has no positive "
+                         "entry, sgp.py:269-270)")
     if np.any(st & STATUS_TEAM_TIMEOUT):
         raise BsgpError(BSGP_ERR_HIP, "team barrier timed out (workgroups not co-resident)")
     if np.any(st & STATUS_LS_CAP):

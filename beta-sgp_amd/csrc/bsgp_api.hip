@@ -383,10 +383,11 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   g.nfw = nfw;
   p->lds_fft_bytes = (size_t)nfw * 2 * g.lpad * sizeof(cd);
   p->lds_bytes = p->lds_fft_bytes + red_bytes;
-  // twiddles of the static-length transforms live in LDS when they fit the
-  // same budget (one table when P == Q); other lengths read the global table
+  // the per-wave transforms' twiddle tables live in LDS when they fit the same
+  // budget (one table when P == Q), else they read the global table (as the
+  // cooperative workgroup-wide transforms always do)
   g.fp.lds_tw = g.fq.lds_tw = -1;
-  if (fft_static_len(g.P) && fft_static_len(g.Q)) {
+  if (!g.coop) {
     const size_t twb = (size_t)(g.P == g.Q ? g.P : g.P + g.Q) * sizeof(cd);
     if (p->lds_bytes + twb <= budget) {
       g.fp.lds_tw = (int)p->lds_bytes;

@@ -209,24 +209,30 @@ BSGP_HD void stage_fixed(const cd* in, cd* out, int n, int Ns, const cd* tw, boo
   }
 }
 
-// Direct-DFT stage for any radix R (used for prime factors > 5).
+// Direct-DFT stage for any radix R (used for prime factors > 5, e.g. the
+// single radix-31 stage of the 31x31 star stamps).  Parallel over the nb*R
+// outputs, not over the nb butterflies: with n = R prime there is ONE
+// butterfly, and a lane per butterfly left 63 of 64 lanes idle through R^2
+// serial multiply-adds.  Each output keeps its summation order (r ascending).
 BSGP_HD void stage_generic(const cd* in, cd* out, int n, int R, int Ns, const cd* tw, bool inv,
                            int lane, int nlanes) {
   const int nb = n / R;
   const int twstep = n / (Ns * R);
   const int rstep = n / R;  // tw[m*rstep] = exp(-2 pi i m / R)
-  for (int j = lane; j < nb; j += nlanes) {
+  for (int q = lane; q < nb * R; q += nlanes) {
+    const int k = q / nb, j = q - k * nb;  // neighbouring lanes: neighbouring butterflies
     const int jm = j % Ns;
     const int od = (j / Ns) * Ns * R + jm;
-    for (int k = 0; k < R; ++k) {
-      cd acc = cmk(0.0, 0.0);
-      for (int r = 0; r < R; ++r) {
-        cd v = in[j + r * nb];
-        if (Ns > 1 && r > 0) v = cmul(v, tw_at(tw, r * jm * twstep, inv));
-        acc = cadd(acc, cmul(v, tw_at(tw, ((r * k) % R) * rstep, inv)));
-      }
-      out[od + k * Ns] = acc;
+    cd acc = cmk(0.0, 0.0);
+    int m = 0;  // (r * k) % R
+    for (int r = 0; r < R; ++r) {
+      cd v = in[j + r * nb];
+      if (Ns > 1 && r > 0) v = cmul(v, tw_at(tw, r * jm * twstep, inv));
+      acc = cadd(acc, cmul(v, tw_at(tw, m * rstep, inv)));
+      m += k;
+      if (m >= R) m -= R;
     }
+    out[od + k * Ns] = acc;
   }
 }
 
@@ -243,14 +249,17 @@ BSGP_HD void fft_stage(const cd* in, cd* out, int n, int R, int Ns, const cd* tw
 
 // Run all stages of `p` on data in `a` (scratch `b`); returns the buffer that
 // holds the result (a or b). `sync()` is called after every stage.
+// `tw`: the plan's twiddle table or a copy of it (LDS); null = p.tw.
 template <class Sync>
-BSGP_HD cd* fft_run(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlanes, Sync sync) {
+BSGP_HD cd* fft_run(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlanes, Sync sync,
+                    const cd* tw = nullptr) {
   cd* in = a;
   cd* out = b;
   int Ns = 1;
+  if (!tw) tw = p.tw;
   for (int s = 0; s < p.ns; ++s) {
     const int R = p.radix[s];
-    fft_stage(in, out, p.n, R, Ns, p.tw, inv, lane, nlanes);
+    fft_stage(in, out, p.n, R, Ns, tw, inv, lane, nlanes);
     sync();
     Ns *= R;
     cd* t = in;
@@ -383,9 +392,9 @@ BSGP_HD cd* fft_wide(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nla
 }
 
 // Runtime length with compile-time fast paths for the hot grid sizes.  On the
-// device the static paths read their twiddles from the LDS copy the kernel
-// made (plan.lds_tw >= 0; LDS latency instead of L1/L2 latency in every
-// butterfly round); other lengths read the global table.
+// device every transform reads its twiddles from the LDS copy the kernel made
+// when the plan placed one (plan.lds_tw >= 0; LDS latency instead of L1/L2
+// latency in every butterfly round), else the global table.
 #if defined(__HIP_DEVICE_COMPILE__)
 extern __shared__ __attribute__((aligned(16))) char bsgp_dyn_lds[];
 #endif
@@ -395,7 +404,8 @@ BSGP_HD cd* fft_any(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlan
   if (p.lds_tw >= 0) {
     const cd* t = reinterpret_cast<const cd*>(bsgp_dyn_lds + p.lds_tw);
     if (p.n == 256) return fft_run_static<256, COMP>(a, b, t, inv, lane, nlanes, sync);
-    return fft_run_static<270, COMP>(a, b, t, inv, lane, nlanes, sync);
+    if (p.n == 270) return fft_run_static<270, COMP>(a, b, t, inv, lane, nlanes, sync);
+    return fft_run(a, b, p, inv, lane, nlanes, sync, t);
   }
   return fft_run(a, b, p, inv, lane, nlanes, sync);
 #else

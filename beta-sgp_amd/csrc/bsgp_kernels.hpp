@@ -46,9 +46,10 @@ namespace bsgp {
 #endif
 // k_ls at 3 waves/SIMD (<= 168 VGPRs; a few spills) with single-column operand
 // batches and plain radix stages in its row passes: +3 % end to end on C3
-// against 2 waves at 216 VGPRs (measured A/B).  Cooperative builds keep 1.
+// against 2 waves at 216 VGPRs (measured A/B).  Cooperative builds keep 1; adaptive beta
+// (the per-trial float32 K and beta derivative) takes 2: 141 spills at 3.
 #ifndef BSGP_LS_ATTR
-#define BSGP_LS_ATTR __attribute__((amdgpu_waves_per_eu(COOP ? 1 : (K <= 2 ? 3 : 2))))
+#define BSGP_LS_ATTR __attribute__((amdgpu_waves_per_eu(COOP ? 1 : ((K <= 2 && !ADAPT) ? 3 : 2))))
 #endif
 #ifndef BSGP_ACC_SERIES
 #define BSGP_ACC_SERIES 0  // den^(b-1) by the series at series-step accepts: same speed on C3 (A/B), off
@@ -365,6 +366,24 @@ __device__ float np_f32_sum(const PwProg& pw, TERM&& term, float* vals, const Pa
   return res;
 }
 
+// Per-image counters of a finished solve (include/bsgp.h bsgp_outputs.counters),
+// written by the image's leader when it stops.
+__device__ __forceinline__ void write_counters(const SolveArgs& A, const ImgState& st, int img,
+                                               int T) {
+  if (!A.out.counters) return;
+  int64_t* c = A.out.counters + (size_t)img * 8;
+  c[0] = st.E_p;
+  c[1] = st.E_ls;
+  c[2] = st.ls_passes;
+  c[3] = st.status |
+         ((A.tfail && __hip_atomic_load(A.tfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ? 4
+                                                                                              : 0);
+  c[4] = st.ls_series;
+  c[5] = T;
+  c[6] = st.proj_passes;
+  c[7] = st.proj_list;
+}
+
 // ------------------------------------------------------------ kernel: setup
 // sgp.py:163-298 (= 617-742): scaling, null pixels, flux, x0, initial
 // projection, x_tf = A(x), f, g and the scaling-matrix bounds.
@@ -611,7 +630,18 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
     st.konst = fsum[0];
     st.g32 = g32;
     st.gfill = fill;
-    atomicAdd(A.active, 1);
+    if (!(ymin < INFINITY)) {
+      // no positive entry in y = flux/(flux+bkg)*AT(gn): the reference's
+      // np.min(y[y > 0]) raises before the first iteration (sgp.py:269-270,
+      // 711-712); the image stops here with status bit 8
+      st.status = 8;
+      st.stop = 1;
+      A.out.iters[img] = 0;
+      if (A.out.beta_final) A.out.beta_final[img] = st.beta;
+      write_counters(A, st, img, tm.T);
+    } else {
+      atomicAdd(A.active, 1);
+    }
   }
 }
 
@@ -1429,19 +1459,7 @@ __device__ __forceinline__ void bb_phase(const SolveArgs& A, int img) {
       st.stop = 1;
       A.out.iters[img] = it2 - 1;
       if (A.out.beta_final) A.out.beta_final[img] = st.beta;
-      if (A.out.counters) {
-        int64_t* c = A.out.counters + (size_t)img * 8;
-        c[0] = st.E_p;
-        c[1] = st.E_ls;
-        c[2] = st.ls_passes;
-        c[3] = st.status |
-               ((A.tfail && __hip_atomic_load(A.tfail, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT)) ? 4 : 0);
-        c[4] = st.ls_series;
-        c[5] = tm.T;
-        c[6] = st.proj_passes;
-        c[7] = st.proj_list;
-      }
+      write_counters(A, st, img, tm.T);
       atomicSub(A.active, 1);
     }
   }
@@ -1589,6 +1607,13 @@ __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs 
           } else {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (need == 0 && A.st[img].stop) {
+              // stopped by the setup (status 8) before its first iteration:
+              // published as stopped for the image's later tasks
+              skip = 1;
+              __hip_atomic_store((gu32*)(done + img), kDoneStop, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+            }
           }
         }
       }

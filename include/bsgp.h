@@ -150,7 +150,9 @@ typedef struct {
   double* beta_final;  /* [B] final betaParam (sgp.py:892), may be NULL           */
   int64_t* counters;   /* [B][8]: proj evals E_p, line-search trials E_ls,
                           line-search passes over the image, status bits (1: line
-                          search cap, 4: team barrier timed out), trials evaluated
+                          search cap, 4: team barrier timed out, 8: no positive
+                          entry in flux/(flux+bkg)*AT(gn), where the reference
+                          raises, sgp.py:269-270), trials evaluated
                           from the small-step series, team size T, projection
                           passes over the image, projection-list entries read;
                           may be NULL */

@@ -45,7 +45,7 @@ static double check_len(int n, bool inv) {
 }
 
 int main() {
-  int lens[] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 16, 25, 31, 32, 60, 64, 96, 100, 128, 243, 256, 270, 288, 300, 320, 384, 512};
+  int lens[] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 14, 16, 25, 31, 32, 49, 62, 77, 93, 60, 64, 96, 100, 128, 243, 256, 270, 288, 300, 320, 384, 512};
   int bad = 0;
   for (int n : lens) {
     for (int inv = 0; inv < 2; ++inv) {

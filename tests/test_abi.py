@@ -122,4 +122,7 @@ def test_check_status_raises_on_status_bits():
     c[1, 3] = 1
     with pytest.raises(_bsgp.BsgpError, match="line search"):
         _bsgp.check_status(c)
+    c[1, 3] = 8  # no positive entry in the scaling bound: the reference's ValueError
+    with pytest.raises(ValueError, match="zero-size array"):
+        _bsgp.check_status(c)
     assert _bsgp.BSGP_ERR_HIP == -2 and _bsgp.BSGP_ERR_ARG == -1

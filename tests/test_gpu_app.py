@@ -278,3 +278,39 @@ def test_line_search_beyond_64_trials_matches_oracle(sgpmod):
     assert it == ito
     assert rel(x, xo) < SOLVE_RTOL, rel(x, xo)
     np.testing.assert_allclose(d, do, rtol=1e-7)
+
+
+@pytest.mark.parametrize("persistent", [0, 1])
+def test_no_positive_scaling_bound_raises_like_reference(sgpmod, persistent):
+    """flux = -bkg/2 makes flux/(flux+bkg) = -1, so y = -AT(gn) has no positive
+    entry and the reference's np.min(y[y > 0]) raises ValueError (sgp.py:269-270
+    / 711-712) before the first iteration: the oracle raises the same and the
+    drop-in raises ValueError; in a batch that image stops at the setup
+    (iters 0, status bit 8) while the others solve as they do alone (phase
+    kernels and the persistent solver)."""
+    import sgp_oracle
+    fx = golden("ref_lin64_beta.npz")
+    kw = ref_kwargs(fx)
+    kw.update(MAXIT=10)
+    gn = fx["gn"].astype(np.float64)
+    with pytest.raises(ValueError):
+        sgp_oracle.sgp_betaDiv(gn, fx["psf"], np.float64(100.0), flux=-50.0, **kw)
+    with pytest.raises(ValueError, match="zero-size array"):
+        sgpmod.sgp_betaDiv(gn, fx["psf"], np.float64(100.0), flux=-50.0, **kw)
+    b = kw.pop("betaParam")
+    f0 = float(np.sum(gn - 100.0))
+    gns = np.stack([gn] * 3)
+    flux = np.array([f0, -50.0, f0])
+    with pytest.raises(ValueError, match=r"image\(s\) \[1\]"):
+        sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, flux=flux, team=1,
+                                 persistent=persistent, betaParams=[b] * 3, **kw)
+    out = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, flux=flux, team=1, persistent=persistent,
+                                   betaParams=[b] * 3, device_out=True, **kw)
+    cnt = out["counters"].cpu().numpy()
+    iters = out["iters"].cpu().numpy()
+    assert iters[1] == 0 and cnt[1, 3] == 8 and cnt[1, 0] == 0
+    one = sgpmod.sgp_betaDiv_batch(gn[None], fx["psf"], 100.0, flux=np.array([f0]), team=1,
+                                   persistent=persistent, betaParams=[b], **kw)
+    for i in (0, 2):
+        assert iters[i] == one["iters"][0] and cnt[i, 3] == 0
+        np.testing.assert_array_equal(out["x"][i].cpu().numpy(), one["x"][0])

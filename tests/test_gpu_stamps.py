@@ -14,7 +14,7 @@ float32 power/log (not correctly rounded).  Two bars:
 * against the oracle with correctly rounded float32 power/log
   (conftest.stamp_oracle_cr, the device's arithmetic): every run, every
   iteration -- equal iteration and line-search trial counts, discrepancy at
-  rtol 1e-9, x within 1e-7, final beta within 1e-10;
+  rtol 1e-6, x within 1e-5, final beta within 1e-10;
 * against the reference (conftest.stamp_parity): the discrepancy up to the
   first iteration whose trial count differs, and x / final beta where all
   trial counts agree.  The runs that part from the reference are exactly the

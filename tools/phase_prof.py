@@ -45,9 +45,17 @@ def main():
     buf = (ctypes.c_uint64 * 32)()
     cfg = bench.CONFIGS[args.config]
     B = args.batch or cfg["batch"]
-    gn, psf = bench.synth_batch(B, cfg["n"], cfg["k"], cfg["nstars"], 0, circular=cfg["circular"])
-    bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
-    kw = bench.solve_kwargs(args.maxit, None, args.streams, None, circular=cfg["circular"])
+    if cfg.get("stamps"):  # the star-stamp workload (bench.py stamps31), phase kernels
+        cuts, psf, bk, fl, betas = bench.stamp_inputs(B)
+        gn = cuts
+        bkg = bk
+        kw = dict(bench.stamp_kwargs(args.maxit), betaParams=betas, flux=fl, streams=args.streams,
+                  persistent=0, team=1)
+    else:
+        gn, psf = bench.synth_batch(B, cfg["n"], cfg["k"], cfg["nstars"], 0,
+                                    circular=cfg["circular"])
+        bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
+        kw = bench.solve_kwargs(args.maxit, None, args.streams, None, circular=cfg["circular"])
     sgp.sgp_betaDiv_batch(gn, psf, bkg, device_out=True, **kw)
     _bsgp.check(L.bsgp_phase_prof(buf, 32, 1))  # reset after warm-up
     out = sgp.sgp_betaDiv_batch(gn, psf, bkg, device_out=True, **kw)
