@@ -83,6 +83,10 @@ CONFIGS = {
     "c5": dict(n=256, k=25, nstars=200, total=8192, circular=False,
                desc="{T} independent {n}x{n} subdivisions split over the GPUs ({B} on this "
                     "rank), 25x25 PSF, linear A"),
+    # the application's subdivision tiles (application_sgp_subdivisions.py:43-107
+    # cuts 375x375 tiles): a 400-point grid, cooperative transforms
+    "sub375": dict(n=375, k=31, nstars=300, batch=512, circular=False,
+                   desc="{B} independent {n}x{n} subdivision-size tiles, 31x31 PSF, linear A"),
     # application_sgp_star_stamps.py:56-105: 31x31 float32 cutouts around stars,
     # the DIAPL PSF with the default circular A, adaptive beta, stop rule 3, the
     # five seeds; the reference's only first-party throughput figure
@@ -469,7 +473,7 @@ def main():
                       f"stop_criterion={kw['stop_criterion']}")
     result = {
         "metric": ("SGP iterations/sec (fp64) on batched 31x31 float32 star stamps" if stamps
-                   else "SGP iterations/sec (fp64) on batched 256x256 images"),
+                   else f"SGP iterations/sec (fp64) on batched {n}x{n} images"),
         "value": value,
         "unit": "image-iterations/s",
         "n_gpus": world,

@@ -376,11 +376,25 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
       delete p;
       return fail(BSGP_ERR_UNSUPPORTED, "FFT length too large for one workgroup's LDS");
     }
-    p->wg_per_cu = (int)(budget / need(1));
+    // thread groups (bsgp_device.hpp, cooperative passes): as many as the LDS
+    // holds, each at least two waves and covering its transform in one load
+    // batch (4 elements per thread).  C4's 2048-point transforms stay on one
+    // group: two groups there measured 6 % slower (A/B); the 400/480-point
+    // grids of the application's subdivisions take four.
+    for (int n = BSGP_COOP_GROUPS; n > 1; n /= 2)
+      if (need(n) <= budget && kCoopBlock / n >= 128 && maxlen <= 4 * (kCoopBlock / n)) {
+        nfw = n;
+        break;
+      }
+    p->wg_per_cu = (int)(budget / need(nfw));
     if (p->wg_per_cu > 4) p->wg_per_cu = 4;
     budget = 160 * 1024 / p->wg_per_cu - 256;
   }
   g.nfw = nfw;
+  // the column kernel of a cooperative plan: BSGP_COOP_COLGROUPS groups (0: as the
+  // other kernels), so it may fit more workgroups per CU than they do
+  g.nfc = (g.coop && BSGP_COOP_COLGROUPS > 0 && BSGP_COOP_COLGROUPS < nfw) ? BSGP_COOP_COLGROUPS
+                                                                            : nfw;
   p->lds_fft_bytes = (size_t)nfw * 2 * g.lpad * sizeof(cd);
   p->lds_bytes = p->lds_fft_bytes + red_bytes;
   // the per-wave transforms' twiddle tables live in LDS when they fit the same
@@ -714,7 +728,7 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   // more workgroups than the team has (C4: 1025 columns, 256-member team)
   a.Tc = T;
   if (T > 1) {
-    const int nc = (p->g.Qh + p->g.nfw - 1) / p->g.nfw;
+    const int nc = (p->g.Qh + p->g.nfc - 1) / p->g.nfc;
     const int want = 4 * p->ncu / B;
     a.Tc = std::max(T, std::min(nc, want));
   }

@@ -61,8 +61,11 @@ struct Geo {
   int H, W;      // image
   int P, Q;      // FFT grid (circular: P=H, Q=W)
   int Qh;        // stored half spectrum width = Q/2 + 1
-  int nfw;       // waves doing FFT work (each owns 2 LDS buffers); 1 in coop mode
-  int coop;      // 1: the whole workgroup runs one transform at a time (long rows/columns)
+  int nfw;       // FFT workers per workgroup, each owning 2 LDS buffers: waves, or in coop
+                 // mode thread groups of kBlock/nfw threads
+  int nfc;       // FFT workers of the column kernel k_col (coop: may be fewer, for more
+                 // workgroups per CU; == nfw otherwise)
+  int coop;      // 1: thread groups of the workgroup run the transforms (long rows/columns)
   int lpad;      // complex elements per LDS buffer (odd: spreads banks)
   FftPlan fp;    // length P (columns)
   FftPlan fq;    // length Q (rows)
@@ -223,9 +226,10 @@ struct Team {
 // chunks of 2*nfw rows (cp pixel pairs) whose row FFTs this member runs, i.e.
 // chunks m, m+T, ...
 struct Part {
-  int gw0, gws;  // first global wave index of this workgroup, global wave stride
+  int gw0, gws;  // first global FFT-worker index of this workgroup, global worker stride
   int gt0, gts;  // first global thread index, global thread stride (strided loops)
   int m, T, cp;  // member, team size, pixel pairs per row chunk
+  int nf;        // FFT workers per workgroup (waves; thread groups in coop mode)
 };
 
 __device__ __forceinline__ Part make_part(const Team& t, int nfw, int W) {
@@ -237,6 +241,7 @@ __device__ __forceinline__ Part make_part(const Team& t, int nfw, int W) {
   d.m = t.m;
   d.T = t.T;
   d.cp = nfw * W;
+  d.nf = nfw;
   return d;
 }
 
@@ -249,6 +254,7 @@ __device__ __forceinline__ Part solo_part(int nfw) {
   d.m = 0;
   d.T = 1;
   d.cp = 0;
+  d.nf = nfw;
   return d;
 }
 
@@ -580,17 +586,30 @@ __device__ __forceinline__ void load_rows(LD& ld, int r, bool two, int j0, int l
 
 // ---------------------------------------------------- cooperative passes
 // Geo::coop: transforms too long for one wave's share of the LDS (the 2048-point
-// rows and columns of config C4) run on the whole workgroup, one row pair or
-// column at a time, 256 lanes per Stockham stage and a workgroup barrier per
-// stage.  The team partition sees the workgroup as a single FFT worker
-// (nfw = 1): member m owns row pairs / columns m, m + T, ...
+// rows and columns of config C4, the 400/480-point grids of the application's
+// subdivisions) run on the whole workgroup or on thread groups of it.
+//
+// One group (Part::nf == 1; C4's 2048-point transforms): one row pair or
+// column at a time, all kBlock lanes per Stockham stage and a workgroup
+// barrier per stage; member m owns row pairs / columns m, m + T, ...
+//
+// Thread groups (nf = 2 or 4; shorter transforms, bsgp_plan_create): nf groups
+// of kBlock/nf threads (whole waves), each with its own pair of LDS buffers,
+// run one row pair or column each; all groups take the same steps through the
+// same barriers (a group with no row pair left in a step transforms its stale
+// buffer and stores nothing).  Worker gw0 + g of the team partition is group
+// g.  A 400-point radix-4 stage has 100 butterflies: one transform per
+// 512-thread workgroup left 80 % of the lanes idle in every stage and ran the
+// row pairs one after the other through the whole latency chain (375^2
+// subdivision tiles: 31.3 k -> 58.6 k image-it/s with four groups, A/B).
 struct BlockSync {
   __device__ __forceinline__ void operator()() const { __syncthreads(); }
 };
 constexpr int kCCH = 4;  // elements per thread per load batch
 
+
 template <class LD, class MK>
-__device__ __forceinline__ void coop_row_fwd(const Geo& G, const Part& D, int nrows, int ncols,
+__device__ __forceinline__ void coop_row_fwd_1(const Geo& G, const Part& D, int nrows, int ncols,
                                              int ldim, cd* spec, cd* lds, LD& ld, MK& mk) {
   using V = decltype(ld(0, 0));
   const int t = threadIdx.x;
@@ -631,7 +650,7 @@ __device__ __forceinline__ void coop_row_fwd(const Geo& G, const Part& D, int nr
   }
 }
 
-__device__ __forceinline__ void coop_gather(const Geo& G, const cd* spec, int r, bool two, cd* a) {
+__device__ __forceinline__ void coop_gather_1(const Geo& G, const cd* spec, int r, bool two, cd* a) {
   const int t = threadIdx.x;
   for (int k0 = 0; k0 < G.Qh; k0 += kBlock * kCCH) {
     cd A[kCCH], B[kCCH];
@@ -656,7 +675,7 @@ __device__ __forceinline__ void coop_gather(const Geo& G, const cd* spec, int r,
 }
 
 template <class LD, class USE>
-__device__ __forceinline__ void coop_row_inv(const Geo& G, const Part& D, const cd* spec, cd* lds,
+__device__ __forceinline__ void coop_row_inv_1(const Geo& G, const Part& D, const cd* spec, cd* lds,
                                              LD& ld, USE& use) {
   using V = decltype(ld(0, 0));
   const int t = threadIdx.x;
@@ -664,7 +683,7 @@ __device__ __forceinline__ void coop_row_inv(const Geo& G, const Part& D, const 
   cd* b = lds + G.lpad;
   for (int r = 2 * D.gw0; r < G.H; r += 2 * D.gws) {
     const bool two = (r + 1) < G.H;
-    coop_gather(G, spec, r, two, a);
+    coop_gather_1(G, spec, r, two, a);
     cd* Z = fft_wide(a, b, G.fq, true, t, kBlock, BlockSync());
     for (int j0 = 0; j0 < G.W; j0 += kBlock * kCCH) {
       V v0[kCCH], v1[kCCH];
@@ -689,7 +708,7 @@ __device__ __forceinline__ void coop_row_inv(const Geo& G, const Part& D, const 
 }
 
 template <class CP>
-__device__ __forceinline__ void coop_row_inv_fwd(const Geo& G, const Part& D, cd* spec, cd* lds,
+__device__ __forceinline__ void coop_row_inv_fwd_1(const Geo& G, const Part& D, cd* spec, cd* lds,
                                                  CP& cp) {
   const int t = threadIdx.x;
   const bool pair_ok = (G.H & 1) == 0;
@@ -697,7 +716,7 @@ __device__ __forceinline__ void coop_row_inv_fwd(const Geo& G, const Part& D, cd
   cd* b = lds + G.lpad;
   for (int r = 2 * D.gw0; r < G.H; r += 2 * D.gws) {
     const bool two = (r + 1) < G.H;
-    coop_gather(G, spec, r, two, a);
+    coop_gather_1(G, spec, r, two, a);
     cd* Z = fft_wide(a, b, G.fq, true, t, kBlock, BlockSync());
     cd* in2 = (Z == a) ? b : a;
     for (int j = t; j < G.Q; j += kBlock) {
@@ -720,7 +739,7 @@ __device__ __forceinline__ void coop_row_inv_fwd(const Geo& G, const Part& D, cd
   }
 }
 
-__device__ __forceinline__ void coop_col_conv(const Geo& G, const Part& D, cd* spec, const cd* tf,
+__device__ __forceinline__ void coop_col_conv_1(const Geo& G, const Part& D, cd* spec, const cd* tf,
                                               cd* lds) {
   const int t = threadIdx.x;
   cd* a = lds;
@@ -759,6 +778,273 @@ __device__ __forceinline__ void coop_col_conv(const Geo& G, const Part& D, cd* s
     for (int p = t; p < G.H; p += kBlock) col[p] = Y[p];
     __syncthreads();
   }
+}
+
+
+struct CGrp {
+  int g, t, nt;  // group, thread in the group, threads per group
+};
+__device__ __forceinline__ CGrp coop_grp(int nf) {
+  const int nt = kBlock / nf;
+  return CGrp{(int)threadIdx.x / nt, (int)threadIdx.x % nt, nt};
+}
+
+template <class LD, class MK>
+__device__ __forceinline__ void coop_row_fwd_g(const Geo& G, const Part& D, int nrows, int ncols,
+                                               int ldim, cd* spec, cd* lds, LD& ld, MK& mk) {
+  using V = decltype(ld(0, 0));
+  const CGrp c = coop_grp(D.nf);
+  const int t = c.t;
+  const bool pair_ok = (ldim & 1) == 0;
+  cd* a = lds + c.g * 2 * G.lpad;
+  cd* b = a + G.lpad;
+  for (int r0 = 2 * D.gw0; r0 < nrows; r0 += 2 * D.gws) {
+    const int r = r0 + 2 * c.g;
+    const bool act = r < nrows;  // uniform in the group
+    const bool two = (r + 1) < nrows;
+    PH_T(tq0);
+    if (act) {
+      for (int j0 = 0; j0 < G.Q; j0 += c.nt * kCCH) {
+        V v0[kCCH], v1[kCCH];
+#pragma unroll
+        for (int u = 0; u < kCCH; ++u) {  // clamped, branch-free (load_rows)
+          const int j = min(j0 + t + c.nt * u, ncols - 1);
+          v0[u] = ld(r, j);
+          v1[u] = ld(two ? r + 1 : r, j);
+        }
+#pragma unroll
+        for (int u = 0; u < kCCH; ++u) {
+          const int j = j0 + t + c.nt * u;
+          if (j < G.Q) {
+            double va = 0.0, vb = 0.0;
+            if (j < ncols) {
+              va = mk(r, j, v0[u]);
+              if (two) vb = mk(r + 1, j, v1[u]);
+            }
+            a[j] = cmk(va, vb);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    PH_ADD(27, tq0);
+    PH_T(tq1);
+    cd* Z = fft_wide(a, b, G.fq, false, t, c.nt, BlockSync());
+    PH_ADD(26, tq1);
+    PH_T(tq2);
+    if (act) {
+      for (int k = t; k < G.Qh; k += c.nt) {
+        cd ak, bk;
+        r2c_split(Z, G.Q, k, &ak, &bk);
+        store_pair(spec + (size_t)k * ldim + r, two, pair_ok, ak, bk);
+      }
+    }
+    __syncthreads();
+    PH_ADD(28, tq2);
+  }
+}
+
+// The full-length spectrum of row pair (r, r+1) from the stored half spectra
+// into `a` (the group's threads); no barrier.
+__device__ __forceinline__ void coop_gather_g(const Geo& G, const cd* spec, int r, bool two, cd* a,
+                                              const CGrp& c) {
+  const int t = c.t;
+  for (int k0 = 0; k0 < G.Qh; k0 += c.nt * kCCH) {
+    cd A[kCCH], B[kCCH];
+#pragma unroll
+    for (int u = 0; u < kCCH; ++u) {  // clamped, branch-free
+      const int k = min(k0 + t + c.nt * u, G.Qh - 1);
+      const cd* col = spec + (size_t)k * G.H + r;
+      A[u] = col[0];
+      const cd b = col[two ? 1 : 0];
+      B[u] = two ? b : cmk(0.0, 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < kCCH; ++u) {
+      const int k = k0 + t + c.nt * u;
+      if (k < G.Qh) {
+        a[k] = cmk(A[u].x - B[u].y, A[u].y + B[u].x);
+        if (k > 0 && G.Q - k >= G.Qh) a[G.Q - k] = cmk(A[u].x + B[u].y, B[u].x - A[u].y);
+      }
+    }
+  }
+}
+
+template <class LD, class USE>
+__device__ __forceinline__ void coop_row_inv_g(const Geo& G, const Part& D, const cd* spec,
+                                               cd* lds, LD& ld, USE& use) {
+  using V = decltype(ld(0, 0));
+  const CGrp c = coop_grp(D.nf);
+  const int t = c.t;
+  cd* a = lds + c.g * 2 * G.lpad;
+  cd* b = a + G.lpad;
+  for (int r0 = 2 * D.gw0; r0 < G.H; r0 += 2 * D.gws) {
+    const int r = r0 + 2 * c.g;
+    const bool act = r < G.H;
+    const bool two = (r + 1) < G.H;
+    PH_T(tq0);
+    if (act) coop_gather_g(G, spec, r, two, a, c);
+    __syncthreads();
+    PH_ADD(25, tq0);
+    PH_T(tq1);
+    cd* Z = fft_wide(a, b, G.fq, true, t, c.nt, BlockSync());
+    PH_ADD(26, tq1);
+    PH_T(tq2);
+    if (act) {
+      for (int j0 = 0; j0 < G.W; j0 += c.nt * kCCH) {
+        V v0[kCCH], v1[kCCH];
+#pragma unroll
+        for (int u = 0; u < kCCH; ++u) {  // clamped, branch-free
+          const int j = min(j0 + t + c.nt * u, G.W - 1);
+          v0[u] = ld(r, j);
+          v1[u] = ld(two ? r + 1 : r, j);
+        }
+#pragma unroll
+        for (int u = 0; u < kCCH; ++u) {
+          const int j = j0 + t + c.nt * u;
+          if (j < G.W) {
+            const cd z = Z[j];
+            use(r, j, z.x, v0[u]);
+            if (two) use(r + 1, j, z.y, v1[u]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    PH_ADD(27, tq2);
+  }
+}
+
+template <class CP>
+__device__ __forceinline__ void coop_row_inv_fwd_g(const Geo& G, const Part& D, cd* spec, cd* lds,
+                                                   CP& cp) {
+  const CGrp c = coop_grp(D.nf);
+  const int t = c.t;
+  const bool pair_ok = (G.H & 1) == 0;
+  cd* a = lds + c.g * 2 * G.lpad;
+  cd* b = a + G.lpad;
+  for (int r0 = 2 * D.gw0; r0 < G.H; r0 += 2 * D.gws) {
+    const int r = r0 + 2 * c.g;
+    const bool act = r < G.H;
+    const bool two = (r + 1) < G.H;
+    PH_T(tq0);
+    if (act) coop_gather_g(G, spec, r, two, a, c);
+    __syncthreads();
+    PH_ADD(25, tq0);
+    PH_T(tq1);
+    cd* Z = fft_wide(a, b, G.fq, true, t, c.nt, BlockSync());
+    cd* in2 = (Z == a) ? b : a;
+    if (act) {
+      for (int j = t; j < G.Q; j += c.nt) {
+        double va = 0.0, vb = 0.0;
+        if (j < G.W) {
+          const cd z = Z[j];
+          va = cp(r, j, z.x);
+          if (two) vb = cp(r + 1, j, z.y);
+        }
+        in2[j] = cmk(va, vb);
+      }
+    }
+    __syncthreads();
+    cd* Y = fft_wide(in2, Z, G.fq, false, t, c.nt, BlockSync());
+    PH_ADD(26, tq1);
+    PH_T(tq2);
+    if (act) {
+      for (int k = t; k < G.Qh; k += c.nt) {
+        cd ak, bk;
+        r2c_split(Y, G.Q, k, &ak, &bk);
+        store_pair(spec + (size_t)k * G.H + r, two, pair_ok, ak, bk);
+      }
+    }
+    __syncthreads();
+    PH_ADD(28, tq2);
+  }
+}
+
+__device__ __forceinline__ void coop_col_conv_g(const Geo& G, const Part& D, cd* spec,
+                                                const cd* tf, cd* lds) {
+  const CGrp c = coop_grp(D.nf);
+  const int t = c.t;
+  cd* a = lds + c.g * 2 * G.lpad;
+  cd* b = a + G.lpad;
+  for (int k0 = D.gw0; k0 < G.Qh; k0 += D.gws) {
+    const int k = k0 + c.g;
+    const bool act = k < G.Qh;
+    cd* col = spec + (size_t)k * G.H;
+    const cd* tk = tf + (size_t)k * G.P;
+    PH_T(tq0);
+    if (act) {
+      for (int p0 = 0; p0 < G.P; p0 += c.nt * kCCH) {
+        cd cv[kCCH];
+#pragma unroll
+        for (int u = 0; u < kCCH; ++u) {  // clamped, branch-free
+          const int p = p0 + t + c.nt * u;
+          const cd v = col[min(p, G.H - 1)];
+          cv[u] = (p < G.H) ? v : cmk(0.0, 0.0);
+        }
+#pragma unroll
+        for (int u = 0; u < kCCH; ++u) {
+          const int p = p0 + t + c.nt * u;
+          if (p < G.P) a[p] = cv[u];
+        }
+      }
+    }
+    __syncthreads();
+    PH_ADD(29, tq0);
+    PH_T(tq1);
+    cd* Z = fft_wide(a, b, G.fp, false, t, c.nt, BlockSync());
+    if (act) {
+      for (int p0 = 0; p0 < G.P; p0 += c.nt * kCCH) {
+        cd tv[kCCH];
+#pragma unroll
+        for (int u = 0; u < kCCH; ++u) tv[u] = tk[min(p0 + t + c.nt * u, G.P - 1)];
+#pragma unroll
+        for (int u = 0; u < kCCH; ++u) {
+          const int p = p0 + t + c.nt * u;
+          if (p < G.P) Z[p] = cmul(Z[p], tv[u]);
+        }
+      }
+    }
+    __syncthreads();
+    cd* Y = fft_wide(Z, (Z == a) ? b : a, G.fp, true, t, c.nt, BlockSync());
+    if (act)
+      for (int p = t; p < G.H; p += c.nt) col[p] = Y[p];
+    __syncthreads();
+    PH_ADD(30, tq1);
+  }
+}
+
+// one group: the whole-workgroup passes; groups: the grouped ones
+template <class LD, class MK>
+__device__ __forceinline__ void coop_row_fwd(const Geo& G, const Part& D, int nrows, int ncols,
+                                             int ldim, cd* spec, cd* lds, LD& ld, MK& mk) {
+  if (D.nf == 1)
+    coop_row_fwd_1(G, D, nrows, ncols, ldim, spec, lds, ld, mk);
+  else
+    coop_row_fwd_g(G, D, nrows, ncols, ldim, spec, lds, ld, mk);
+}
+template <class LD, class USE>
+__device__ __forceinline__ void coop_row_inv(const Geo& G, const Part& D, const cd* spec, cd* lds,
+                                             LD& ld, USE& use) {
+  if (D.nf == 1)
+    coop_row_inv_1(G, D, spec, lds, ld, use);
+  else
+    coop_row_inv_g(G, D, spec, lds, ld, use);
+}
+template <class CP>
+__device__ __forceinline__ void coop_row_inv_fwd(const Geo& G, const Part& D, cd* spec, cd* lds,
+                                                 CP& cp) {
+  if (D.nf == 1)
+    coop_row_inv_fwd_1(G, D, spec, lds, cp);
+  else
+    coop_row_inv_fwd_g(G, D, spec, lds, cp);
+}
+__device__ __forceinline__ void coop_col_conv(const Geo& G, const Part& D, cd* spec, const cd* tf,
+                                              cd* lds) {
+  if (D.nf == 1)
+    coop_col_conv_1(G, D, spec, tf, lds);
+  else
+    coop_col_conv_g(G, D, spec, tf, lds);
 }
 
 // row_fwd2: for every pair of image rows (r, r+1) one wave FFTs z = a + i b

@@ -130,6 +130,15 @@ void persist_kernels_all(std::vector<const void*>& f);
 // Cooperative plans (Geo::coop) run the phase kernels of bsgp_solver_c512.hip:
 // the same kernels with 512-thread workgroups (two waves per SIMD per
 // workgroup where a long transform's LDS allows one or two workgroups per CU).
+// cooperative plans: at most this many thread groups per workgroup run
+// transforms side by side (bsgp_device.hpp coop passes), and the column
+// kernel's groups (0: the same as the other kernels)
+#ifndef BSGP_COOP_GROUPS
+#define BSGP_COOP_GROUPS 4
+#endif
+#ifndef BSGP_COOP_COLGROUPS
+#define BSGP_COOP_COLGROUPS 1
+#endif
 #ifndef BSGP_COOP512
 #define BSGP_COOP512 1
 #endif

@@ -960,7 +960,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_COL_ATTR k_col(SolveArgs A, int t
   tm.m = A.Tc == 1 ? 0 : (int)(blockIdx.x % (unsigned)A.Tc);
   const Bufs<double> B = slot_bufs<double>(A, img, 0);  // spec only (same offset for V)
   load_tw_lds(A.g);
-  col_conv<COOP>(A.g, make_part(tm, A.g.nfw, A.g.W), B.spec, tf_of(A.g, img, transpose), lds);
+  col_conv<COOP>(A.g, make_part(tm, A.g.nfc, A.g.W), B.spec, tf_of(A.g, img, transpose), lds);
   PH_ADD(3, tc0);
 }
 
@@ -1780,7 +1780,14 @@ inline hipError_t launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipS
   if (ev) chk(hipEventRecord(ev[0], s));
   chk(launch_fn((const void*)k_dir<COOP, V>, grid, lds, s, a));
   if (ev) chk(hipEventRecord(ev[1], s));
-  if (!(a.fuse_col & 5)) chk(launch_fn((const void*)k_col<COOP>, gcol, lds, s, a, 0));
+  // k_col of a cooperative plan needs only its own groups' buffers (no
+  // reduction scratch, no LDS twiddles)
+#ifndef BSGP_COL_LDS_FULL
+#define BSGP_COL_LDS_FULL 0
+#endif
+  const size_t lds_col =
+      (COOP && !BSGP_COL_LDS_FULL) ? (size_t)a.g.nfc * 2 * a.g.lpad * sizeof(cd) : lds;
+  if (!(a.fuse_col & 5)) chk(launch_fn((const void*)k_col<COOP>, gcol, lds_col, s, a, 0));
   if (ev) chk(hipEventRecord(ev[2], s));
   // line-search kernel specialised on trial width, objective mode, adaptivity
   const bsgp_params& P = a.prm;
@@ -1789,7 +1796,7 @@ inline hipError_t launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipS
   const int mode = P.variant == BSGP_VARIANT_KL ? 0 : special ? -1 : P.gn_f32 ? 4 : 3;
   chk(launch_fn(ls_kernel<COOP, V>(K, mode, adapt), grid, lds, s, a));
   if (ev) chk(hipEventRecord(ev[3], s));
-  if (!(a.fuse_col & 2)) chk(launch_fn((const void*)k_col<COOP>, gcol, lds, s, a, 1));
+  if (!(a.fuse_col & 2)) chk(launch_fn((const void*)k_col<COOP>, gcol, lds_col, s, a, 1));
   if (ev) chk(hipEventRecord(ev[4], s));
   chk(launch_fn((const void*)k_bb<COOP, V>, grid, lds, s, a));
   if (ev) chk(hipEventRecord(ev[5], s));

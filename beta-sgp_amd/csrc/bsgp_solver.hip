@@ -73,19 +73,24 @@ __global__ void __launch_bounds__(kBlock) tf_cols_kernel(Geo G, const cd* spec,
   tf += blockIdx.y * tf_stride;
   load_tw_lds(G);
   if constexpr (COOP) {
-    const int t = threadIdx.x;
-    cd* a = lds;
-    cd* b = lds + G.lpad;
-    for (int k = blockIdx.x; k < G.Qh; k += gridDim.x) {
+    // thread groups as the solver's cooperative passes (coop_col_conv)
+    const CGrp c = coop_grp(G.nfw);
+    cd* a = lds + c.g * 2 * G.lpad;
+    cd* b = a + G.lpad;
+    for (int k0 = blockIdx.x * G.nfw; k0 < G.Qh; k0 += gridDim.x * G.nfw) {
+      const int k = k0 + c.g;
+      const bool act = k < G.Qh;
       const cd* col = spec + (size_t)k * G.P;
-      for (int p = t; p < G.P; p += kBlock) a[p] = col[p];
+      if (act)
+        for (int p = c.t; p < G.P; p += kBlock / G.nfw) a[p] = col[p];
       __syncthreads();
-      cd* Z = fft_wide(a, b, G.fp, false, t, kBlock, BlockSync());
+      cd* Z = fft_wide(a, b, G.fp, false, c.t, kBlock / G.nfw, BlockSync());
       cd* o = tf + (size_t)k * G.P;
-      for (int p = t; p < G.P; p += kBlock) {
-        const cd z = cscale(Z[p], scale);
-        o[p] = conj ? cconj(z) : z;
-      }
+      if (act)
+        for (int p = c.t; p < G.P; p += kBlock / G.nfw) {
+          const cd z = cscale(Z[p], scale);
+          o[p] = conj ? cconj(z) : z;
+        }
       __syncthreads();
     }
   } else {

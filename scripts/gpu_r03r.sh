@@ -1,0 +1,10 @@
+#!/bin/bash
+# Coop groups for short transforms only: GPU suite, then A/B on C4 f32 and sub375.
+set -o pipefail
+TAG=${1:-r03r}
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf -p no:cacheprovider --timeout 240 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
+rc=$?; echo "TESTS EXIT $rc"; grep -E "FAILED|ERROR" gpurun_out/${TAG}_tests.log | head -20; tail -2 gpurun_out/${TAG}_tests.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+bash scripts/gpu_ab.sh ${TAG}_c4f32 3 old base -- --config c4 --storage f32 --steps 10 --no-e2e || exit $?
+bash scripts/gpu_ab.sh ${TAG}_sub375 2 old base -- --config sub375 --maxit 50 --steps 2 --no-e2e

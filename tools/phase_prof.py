@@ -25,7 +25,9 @@ SLOTS = {0: "k_dir projection", 1: "k_dir row pass", 2: "k_dir total", 3: "k_col
          13: "  ls1 rows: operand batches", 14: "  ls1 rows: FFT", 15: "  ls1 rows: stage/unpack",
          16: "  accept rows: operand batches", 17: "  accept rows: FFT", 18: "  accept rows: stores",
          19: "  bb rows: operand batches", 20: "  bb rows: FFT", 21: "  bb rows: stage/unpack",
-         22: "  dir rows: operand batches", 23: "  dir rows: FFT", 24: "  dir rows: stores"}
+         22: "  dir rows: operand batches", 23: "  dir rows: FFT", 24: "  dir rows: stores",
+         25: "  coop rows: spectrum gathers", 26: "  coop rows: FFTs", 27: "  coop rows: operands",
+         28: "  coop rows: spectrum stores", 29: "  coop cols: loads", 30: "  coop cols: FFT+TF+store"}
 
 
 def main():
