@@ -335,25 +335,42 @@ __device__ float np_f32_sum(const PwProg& pw, TERM&& term, float* vals, const Pa
   const int* nd = lv + 2 * pw.nleaf;
   const int* off = nd + 2 * pw.nnode;
   const int* roots = off + pw.nlev + 1;
-  for (int l = D.gt0 + (int)threadIdx.x; l < pw.nleaf; l += D.gts) {
-    const int s0 = lv[2 * l], n = lv[2 * l + 1];
-    float res;
-    if (n < 8) {
-      res = 0.0f;
-      for (int i = 0; i < n; ++i) res += term(s0 + i);
-    } else {
-      float r[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = term(s0 + j);
-      int i = 8;
-      for (; i < n - (n % 8); i += 8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] += term(s0 + i + j);
-      }
-      res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-      for (; i < n; ++i) res += term(s0 + i);
+  // A leaf's 8 accumulators on 8 neighbouring lanes: lane j of the leaf's lane
+  // group sums terms j, j+8, ... in order, the group folds them as numpy does,
+  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), by xor-shuffles (a+b == b+a bit for
+  // bit), and its lane 0 adds the n % 8 tail in order.  One lane per leaf ran
+  // 8x longer chains (a 961-pixel stamp: 8 leaves of up to 128 float32 powers
+  // on 8 lanes of the workgroup, at every trial of adaptive beta).
+  const int q = D.gt0 + (int)threadIdx.x;
+  const int j = q & 7;
+  const int lstride = D.gts >> 3;
+  const int nrounds = (pw.nleaf + lstride - 1) / lstride;  // the same in every lane
+  for (int it = 0; it < nrounds; ++it) {
+    const int l = (q >> 3) + it * lstride;
+    const bool act = l < pw.nleaf;
+    const int s0 = act ? lv[2 * l] : 0, n = act ? lv[2 * l + 1] : 0;
+    float r = 0.0f;
+    if (n >= 8) {
+      const int m8 = n - (n % 8);
+      r = term(s0 + j);
+      for (int i = 8 + j; i < m8; i += 8) r += term(s0 + i);
     }
-    vals[l] = res;
+    float s = r + __shfl_xor(r, 1);
+    s = s + __shfl_xor(s, 2);
+    s = s + __shfl_xor(s, 4);
+    if (act && j == 0) {
+      float res;
+      int i;
+      if (n < 8) {
+        res = 0.0f;
+        i = 0;
+      } else {
+        res = s;
+        i = n - (n % 8);
+      }
+      for (; i < n; ++i) res += term(s0 + i);
+      vals[l] = res;
+    }
   }
   team_sync(tm);
   for (int h = 0; h < pw.nlev; ++h) {
