@@ -12,5 +12,5 @@ for C in "$P1" "$P2"; do
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $C -d gpurun_out/${TAG}_p$i -o run --output-format csv \
     -- python bench.py --no-cpu --streams 1 --steps 1 --warmup 0 --maxit 20 "$@" > gpurun_out/${TAG}_p$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 gpurun_out/${TAG}_p$i.log; exit 3; }
   F=$(find gpurun_out/${TAG}_p$i -name "*counter_collection.csv" | head -1)
-  python tools/pmc_summary.py $F | grep -E "k_dir|k_col|k_ls|k_bb"
+  python tools/pmc_summary.py $F | grep -E "k_dir|k_col|k_ls|k_bb|k_persist"
 done
