@@ -802,7 +802,7 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     if (track) HIP_TRY(launch_track(sa[j], 0, ss[j]));
   }
   if (persist) {
-    const size_t need = (size_t)B + 1;  // queue word + done[B]
+    const size_t need = (size_t)2 * B + 4;  // head, tail, pad, ready ring[B] (64-bit entries)
     if (need > p->pq_n) {
       if (p->pq) HIP_TRY(hipFree(p->pq));
       p->pq = nullptr;

@@ -125,6 +125,7 @@ hipError_t phase_prof(unsigned long long* out, int n, int reset);
 hipError_t launch_persist(const SolveArgs& a, int K, size_t lds, hipStream_t s, unsigned* queue,
                           unsigned* done, int grid);
 hipError_t persist_resident_per_cu(const SolveArgs& a, int K, size_t lds, int* per_cu);
+hipError_t persist_phase_prof(unsigned long long* out, int n, int reset);
 void persist_kernels_all(std::vector<const void*>& f);
 
 // Cooperative plans (Geo::coop) run the phase kernels of bsgp_solver_c512.hip:

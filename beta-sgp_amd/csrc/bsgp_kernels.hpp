@@ -1492,36 +1492,53 @@ __global__ void __launch_bounds__(kBlock) k_bb(SolveArgs A) {
 
 // ------------------------------------------- persistent task-queue solver
 // One-workgroup images with per-wave transforms (T == 1, the batched configs
-// C3/C5): ONE launch runs every iteration of every image of a sub-batch.  A
-// task is (iteration k, image i); tasks are dequeued in the order t = (k-1) *
-// nimg + (i - img0) from one device counter, so every resident workgroup has
-// work until the last iteration's tasks and no launch ends in a
-// partly-occupied round (1024 images on 768 slots are 1.33 rounds per
-// launch in the phase-kernel solve), and a CU holds workgroups in different
-// phases of their tasks at once (memory-bound row passes beside LDS-bound
-// transforms).  A task runs the phases of one iteration (dir_phase, A's
-// column pass, ls_phase with AT's column pass, bb_phase), the same device code
-// the phase kernels run, so the results are bit-identical to theirs.
+// C3/C5 and the star stamps): ONE launch runs every iteration of every image
+// of a sub-batch.  A task is one iteration of one image.  Images wait in a
+// ready ring: a workgroup takes the entry at the ring's head, runs one
+// iteration of that image and, unless the image stopped, appends it at the
+// tail.  So every resident workgroup has work until the last iterations, no
+// launch ends in a partly-occupied round (1024 images on 768 slots are 1.33
+// rounds per launch in the phase-kernel solve), a CU holds workgroups in
+// different phases of their tasks at once (memory-bound row passes beside
+// LDS-bound transforms), and a stopped image costs nothing more (the star
+// stamps stop after ~20 of MAXIT 500 iterations at different times: with one
+// task per (iteration, image) slot, the slots of stopped images were still
+// dequeued and skipped one by one, 15 % of the stamp solve).  A task runs the
+// phases of one iteration (dir_phase, A's column pass, ls_phase with AT's
+// column pass, bb_phase), the same device code the phase kernels run, so the
+// results are bit-identical to theirs.  Solves with a data-dependent stop
+// rule (2-4) take the ring; fixed-length solves take the slot order below.
 //
-// Iteration k of image i needs iteration k - 1 done, usually by another
-// workgroup on another CU or XCD.  Hand-off (MI355X_MICROARCH.md,
+// Ring (queue[0] = head, queue[1] = tail, then ring[nimg] of 64-bit entries
+// (h << 32 | image) for position h; k_ring_init fills positions 0..nimg-1):
+// an image is in the ring at most once, so the entries written and not yet
+// read are distinct images, at most nimg, and position h + nimg is never
+// written before position h has been read.  Hand-off (MI355X_MICROARCH.md,
 // inter-workgroup visibility, valid producer/consumer forms): the producer's
 // waves drain their stores, a workgroup barrier, lane 0 releases at agent
-// scope and stores done[i] = k with a relaxed agent-scope (sc1) store; the
-// consumer's lane 0 polls done[i] with sc1 loads, acquires at agent scope,
-// and a workgroup barrier lets the other waves load.  The predecessor task
-// was dequeued earlier by a resident workgroup, so the wait always ends; the
-// poll is bounded anyway (timeout -> status bit 4, every workgroup leaves).
-// An image that stopped publishes kDoneStop | k: its later tasks are skipped
-// without a fence.  When no image is running the workgroups leave early.
-constexpr unsigned kDoneStop = 0x40000000u;
+// scope, takes a tail position with an atomic add and stores the entry with a
+// relaxed agent-scope (sc1) 64-bit store; the consumer's lane 0 polls its
+// position with sc1 loads until the entry carries that position, acquires at
+// agent scope, and a workgroup barrier lets the other waves load.  A consumer
+// whose position is never written (every image stopped) sees the running
+// count at 0 and leaves; the poll is bounded anyway (timeout -> status bit 4,
+// every workgroup leaves).
+static __global__ void k_ring_init(unsigned* queue, int nimg, int img0) {
+  unsigned long long* ring = reinterpret_cast<unsigned long long*>(queue + 4);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {
+    queue[0] = 0;
+    queue[1] = (unsigned)nimg;
+  }
+  if (i < nimg) ring[i] = ((unsigned long long)i << 32) | (unsigned)(img0 + i);
+}
 
 #ifndef BSGP_PERSIST_ATTR
 #define BSGP_PERSIST_ATTR __attribute__((amdgpu_waves_per_eu(3)))
 #endif
 
-__device__ __forceinline__ unsigned ld_sc1_u32(const unsigned* p) {
-  return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long long* p) {
+  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The phases of a task are separate (noinline) functions, so each keeps the
@@ -1584,66 +1601,110 @@ __device__ BSGP_PERSIST_FN void persist_bb(ArgRef r, int img) {
   bb_phase<false, V>(args_of(r), __builtin_amdgcn_readfirstlane(img));
 }
 
+// Slot order (fixed-length solves, stop rules 0/1): task t = (k - 1) * nimg + i
+// runs iteration k of image i, dequeued from one counter; iteration k waits
+// for done[i] >= k - 1 (published as below with a 32-bit sc1 store).  Every
+// image runs every iteration, so no slot is ever skipped, and the iterations
+// of all images advance in lock step (C3: the ring's completion order was
+// 5 % slower, A/B).  Data-dependent stop rules (2-4) take the ready ring.
+constexpr unsigned kDoneStop = 0x40000000u;
+__device__ __forceinline__ unsigned ld_sc1_u32(const unsigned* p) {
+  return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int K, int MODE, bool ADAPT, class V>
 __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs A,
                                                                         unsigned* queue,
                                                                         unsigned* done) {
   BSGP_LDS_VIEWS(A);
   (void)red;
-  __shared__ unsigned s_task, s_skip;
+  __shared__ int s_img;
+  __shared__ unsigned s_k;
   const int tid = threadIdx.x;
   const Geo& G = A.g;
   load_tw_lds(G);
   const unsigned nimg = (unsigned)A.nimg;
   const unsigned total = (unsigned)A.prm.MAXIT * nimg;
+  const bool use_ring = A.prm.stop_criterion >= 2 && A.prm.stop_criterion <= 4;
+  unsigned long long* ring = reinterpret_cast<unsigned long long*>(queue + 4);
   for (;;) {
+    PH_T(tq);
     if (tid == 0) {
-      unsigned t = atomicAdd(queue, 1u);
-      unsigned skip = 0;
-      if (t < total && __hip_atomic_load((gi32*)A.active, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT) <= 0)
-        t = total;  // every image has stopped: nothing left to run
-      if (t < total) {
-        const int img = A.img0 + (int)(t % nimg);
-        const unsigned need = t / nimg;  // iterations of img that must be done
-        unsigned d = ld_sc1_u32(done + img), spins = 0;
-        while (d < need) {
+      int img = -1;  // -1: leave, -2: nothing to run for this entry
+      unsigned k = 0;
+      if (use_ring) {
+        const unsigned h = atomicAdd(queue, 1u);
+        unsigned long long e = ld_sc1_u64(ring + h % nimg);
+        unsigned spins = 0;
+        while ((unsigned)(e >> 32) != h) {
           __builtin_amdgcn_s_sleep(2);
-          d = ld_sc1_u32(done + img);
-          if ((++spins & 1023u) == 0 &&
-              (__hip_atomic_load((gi32*)A.tfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
-               spins > (1u << 26))) {
-            __hip_atomic_store((gi32*)A.tfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            t = total;
-            break;
+          if ((++spins & 63u) == 0) {
+            if (__hip_atomic_load((gi32*)A.active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <=
+                0)
+              break;  // every image has stopped: position h is never written
+            if (__hip_atomic_load((gi32*)A.tfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+                spins > (1u << 26)) {
+              __hip_atomic_store((gi32*)A.tfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
           }
+          e = ld_sc1_u64(ring + h % nimg);
         }
+        if ((unsigned)(e >> 32) == h) {
+          img = (int)(unsigned)e;
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          // stopped by the setup (status 8) before its first iteration: it
+          // leaves the ring (the setup did not count it as running)
+          if (A.st[img].stop) img = -2;
+        }
+      } else {
+        unsigned t = atomicAdd(queue, 1u);
+        if (t < total && __hip_atomic_load((gi32*)A.active, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT) <= 0)
+          t = total;  // every image has stopped: nothing left to run
         if (t < total) {
-          if (d & kDoneStop) {
-            skip = 1;  // stopped: nothing of this image is read or written
-          } else {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (need == 0 && A.st[img].stop) {
-              // stopped by the setup (status 8) before its first iteration:
-              // published as stopped for the image's later tasks
-              skip = 1;
-              __hip_atomic_store((gu32*)(done + img), kDoneStop, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+          img = A.img0 + (int)(t % nimg);
+          const unsigned need = t / nimg;  // iterations of img that must be done
+          k = need + 1;
+          unsigned d = ld_sc1_u32(done + img), spins = 0;
+          while (d < need) {
+            __builtin_amdgcn_s_sleep(2);
+            d = ld_sc1_u32(done + img);
+            if ((++spins & 1023u) == 0 &&
+                (__hip_atomic_load((gi32*)A.tfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+                 spins > (1u << 26))) {
+              __hip_atomic_store((gi32*)A.tfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              img = -1;
+              break;
+            }
+          }
+          if (img >= 0) {
+            if (d & kDoneStop) {
+              img = -2;  // stopped: nothing of this image is read or written
+            } else {
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+              if (need == 0 && A.st[img].stop) {
+                // stopped by the setup (status 8): published as stopped
+                __hip_atomic_store((gu32*)(done + img), kDoneStop, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                img = -2;
+              }
             }
           }
         }
       }
-      s_task = t;
-      s_skip = skip;
+      s_img = img;
+      s_k = k;
     }
     __syncthreads();
-    const unsigned t = s_task;
-    const bool skip = s_skip != 0;
-    __syncthreads();  // s_task is rewritten by lane 0 only after every wave has read it
-    if (t >= total) break;
-    if (skip) continue;
-    const int img = A.img0 + (int)(t % nimg);
+    const int img = s_img;
+    const unsigned k = s_k;
+    __syncthreads();  // s_img is rewritten by lane 0 only after every wave has read it
+    PH_ADD(31, tq);  // dequeue + wait for an image
+    if (img == -1) break;
+    if (img < 0) continue;
     const ArgRef ar = kernarg_ref();
     persist_dir<V>(ar, img);
     __syncthreads();  // rows of d and the direction scalars complete
@@ -1651,16 +1712,27 @@ __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs 
     persist_ls<K, MODE, ADAPT, V>(ar, img);
     __syncthreads();  // the accepted step and AT's columns complete
     persist_bb<V>(ar, img);
-    // publish iteration k of img: every wave's stores drained, then lane 0
-    // releases at agent scope and stores the flag (sc1)
+    // hand the image on: every wave's stores drained, then lane 0 releases at
+    // agent scope and publishes (sc1 store): ring append, or done[img]
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      const unsigned k = t / nimg + 1;
-      const unsigned flag = A.st[img].stop ? (kDoneStop | k) : k;  // lane 0 is bb's leader
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store((gu32*)(done + img), flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool stopped = A.st[img].stop != 0;  // lane 0 is bb's leader: its own write
+      if (use_ring) {
+        if (!stopped) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          const unsigned t = atomicAdd(queue + 1, 1u);
+          __hip_atomic_store((gu64*)(ring + t % nimg),
+                             ((unsigned long long)t << 32) | (unsigned)img, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store((gu32*)(done + img), stopped ? (kDoneStop | k) : k, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 }
@@ -1687,6 +1759,9 @@ inline void persist_kernels(std::vector<const void*>& f) {
 template <class V>
 inline hipError_t launch_persist_t(const SolveArgs& a, int K, size_t lds, hipStream_t s,
                                    unsigned* queue, unsigned* done, int grid) {
+  if (a.prm.stop_criterion >= 2 && a.prm.stop_criterion <= 4)
+    hipLaunchKernelGGL(k_ring_init, dim3((a.nimg + 255) / 256), dim3(256), 0, s, queue, a.nimg,
+                       a.img0);
   const bsgp_params& P = a.prm;
   const bool adapt = P.adapt_beta && P.variant == BSGP_VARIANT_BETA;
   const bool special = a.in.beta0 ? !P.beta0_general : (P.betaParam == 0.0 || P.betaParam == 1.0);

@@ -40,6 +40,29 @@ hipError_t persist_resident_per_cu(const SolveArgs& a, int K, size_t lds, int* p
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, f, kBlock, lds);
 }
 
+// phase-profile counters of this translation unit's kernels (-DBSGP_PHASE_PROF;
+// phase_prof in bsgp_solver.hip adds them)
+hipError_t persist_phase_prof_f32(unsigned long long* out, int n, int reset);
+hipError_t persist_phase_prof(unsigned long long* out, int n, int reset) {
+#ifdef BSGP_PHASE_PROF
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), n * sizeof(unsigned long long));
+  if (e == hipSuccess && reset) {
+    unsigned long long z[kPhaseSlots] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z);
+  }
+  if (e == hipSuccess) {
+    unsigned long long c[kPhaseSlots] = {};
+    e = persist_phase_prof_f32(c, n, reset);
+    for (int i = 0; i < n; ++i) out[i] += c[i];
+  }
+  return e;
+#else
+  for (int i = 0; i < n; ++i) out[i] = 0;
+  (void)reset;
+  return hipSuccess;
+#endif
+}
+
 void persist_kernels_all(std::vector<const void*>& f) {
   persist_kernels<double>(f);
   persist_kernels_f32(f);

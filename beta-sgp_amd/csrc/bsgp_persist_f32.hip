@@ -16,5 +16,19 @@ const void* persist_kernel_f32(int K, int mode, bool adapt) {
   return persist_kernel<float>(K, mode, adapt);
 }
 void persist_kernels_f32(std::vector<const void*>& f) { persist_kernels<float>(f); }
+hipError_t persist_phase_prof_f32(unsigned long long* out, int n, int reset) {
+#ifdef BSGP_PHASE_PROF
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), n * sizeof(unsigned long long));
+  if (e == hipSuccess && reset) {
+    unsigned long long z[kPhaseSlots] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z);
+  }
+  return e;
+#else
+  for (int i = 0; i < n; ++i) out[i] = 0;
+  (void)reset;
+  return hipSuccess;
+#endif
+}
 
 }  // namespace bsgp

@@ -32,6 +32,13 @@ hipError_t phase_prof(unsigned long long* out, int n, int reset) {
     if (e == hipSuccess && out)
       for (int i = 0; i < n; ++i) out[i] += c[i];
   }
+  // and so do the persistent solver's translation units
+  if (e == hipSuccess) {
+    unsigned long long c[kPhaseSlots] = {};
+    e = persist_phase_prof(c, n, reset);
+    if (e == hipSuccess && out)
+      for (int i = 0; i < n; ++i) out[i] += c[i];
+  }
   return e;
 #else
   (void)out;

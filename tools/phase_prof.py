@@ -27,7 +27,8 @@ SLOTS = {0: "k_dir projection", 1: "k_dir row pass", 2: "k_dir total", 3: "k_col
          19: "  bb rows: operand batches", 20: "  bb rows: FFT", 21: "  bb rows: stage/unpack",
          22: "  dir rows: operand batches", 23: "  dir rows: FFT", 24: "  dir rows: stores",
          25: "  coop rows: spectrum gathers", 26: "  coop rows: FFTs", 27: "  coop rows: operands",
-         28: "  coop rows: spectrum stores", 29: "  coop cols: loads", 30: "  coop cols: FFT+TF+store"}
+         28: "  coop rows: spectrum stores", 29: "  coop cols: loads", 30: "  coop cols: FFT+TF+store",
+         31: "persistent: dequeue + wait for the previous iteration"}
 
 
 def main():
@@ -36,6 +37,8 @@ def main():
     ap.add_argument("--maxit", type=int, default=20)
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--config", default="c3")
+    ap.add_argument("--persistent", type=int, default=None,
+                    help="1: the persistent solver (default for c3; stamps default 0)")
     args = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime, loaded before the library)
     import bench
@@ -52,12 +55,13 @@ def main():
         gn = cuts
         bkg = bk
         kw = dict(bench.stamp_kwargs(args.maxit), betaParams=betas, flux=fl, streams=args.streams,
-                  persistent=0, team=1)
+                  persistent=args.persistent or 0, team=1)
     else:
         gn, psf = bench.synth_batch(B, cfg["n"], cfg["k"], cfg["nstars"], 0,
                                     circular=cfg["circular"])
         bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
-        kw = bench.solve_kwargs(args.maxit, None, args.streams, None, circular=cfg["circular"])
+        kw = bench.solve_kwargs(args.maxit, None, args.streams, None, circular=cfg["circular"],
+                                persistent=args.persistent)
     sgp.sgp_betaDiv_batch(gn, psf, bkg, device_out=True, **kw)
     _bsgp.check(L.bsgp_phase_prof(buf, 32, 1))  # reset after warm-up
     out = sgp.sgp_betaDiv_batch(gn, psf, bkg, device_out=True, **kw)
