@@ -233,6 +233,16 @@ class Plan:
         M1 = params.MAXIT + 1
         dev = gn.device
         f64 = dict(dtype=torch.float64, device=dev)
+        if want_iterates:
+            # save=True keeps every iterate of the MAXIT budget on the device
+            # (copied to the host once, up to the iterations run): refuse a
+            # budget that the device cannot hold beside the solve's own workspace
+            need = B * params.MAXIT * self.H * self.W * 8
+            free = torch.cuda.mem_get_info(dev)[0]
+            if need > 0.8 * free:
+                raise BsgpError(
+                    f"save=True keeps {params.MAXIT} iterates of {self.H}x{self.W} on the device "
+                    f"({need / 2**30:.1f} GiB, {free / 2**30:.1f} GiB free): lower MAXIT")
         out = {
             "x": torch.empty_like(gn),
             "iters": torch.zeros(B, dtype=torch.int32, device=dev),

@@ -732,7 +732,10 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     const int want = 4 * p->ncu / B;
     a.Tc = std::max(T, std::min(nc, want));
   }
-  a.fuse_col = T == 1 ? BSGP_FUSE_COL : 0;
+  // column passes fused into the row kernels: one-workgroup images always;
+  // teams of per-wave plans as BSGP_FUSE_COL_TEAM says (the team's own waves
+  // run the columns after a team barrier, instead of a k_col launch)
+  a.fuse_col = T == 1 ? BSGP_FUSE_COL : (p->g.coop ? 0 : BSGP_FUSE_COL_TEAM);
   a.tpart = T > 1 ? p->tpart : nullptr;
   a.tctr = p->tctr;
   a.tfail = reinterpret_cast<int*>(p->tctr + (size_t)B * kTeamWords);

@@ -39,6 +39,14 @@ struct ImgState {
 #ifndef BSGP_FUSE_COL
 #define BSGP_FUSE_COL 2
 #endif
+// teams of per-wave plans (C2): which column passes their row kernels run
+// after a team barrier instead of a k_col launch
+#ifndef BSGP_FUSE_COL_TEAM
+#define BSGP_FUSE_COL_TEAM 0
+#endif
+// fused-column code compiled into the kernels (a pass not compiled in costs no
+// registers in the kernels that never run it)
+#define BSGP_FUSE_COL_CODE (BSGP_FUSE_COL | BSGP_FUSE_COL_TEAM)
 
 // numpy float32 reduction program of a plan's N (bsgp_api.hip pairwise_program):
 // [nleaf][2] leaves (start, len), [nnode][2] node operands (value indices),

@@ -934,7 +934,7 @@ __device__ __forceinline__ void dir_phase(const SolveArgs& A, int img) {
       });
   team_sum<1>(gd, red, tm);
   PH_ADD(1, tk1);
-  if ((BSGP_FUSE_COL & 1) && (A.fuse_col & 1)) {  // T == 1: A's column pass follows here
+  if ((BSGP_FUSE_COL_CODE & 1) && (A.fuse_col & 1)) {  // A's column pass follows here
     PH_T(tc0);
     team_sync(tm);
     col_conv<COOP>(G, Pt, B.spec, tf_of(G, img, 0), lds);
@@ -1004,7 +1004,7 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
   const double lr_st = st.lr;
   constexpr bool adapt = ADAPT;  // adaptive beta (sgp.py:798-800): K == 1, runtime mode
   Bufs<V> B = slot_bufs<V>(A, img, st.par);
-  if ((BSGP_FUSE_COL & 4) && (A.fuse_col & 4)) {  // T == 1: A's column pass of k_dir's rows
+  if ((BSGP_FUSE_COL_CODE & 4) && (A.fuse_col & 4)) {  // A's column pass of k_dir's rows
     PH_T(tc0);
     col_conv<COOP>(G, Pt, B.spec, tf_of(G, img, 0), lds);
     team_sync(tm);
@@ -1311,7 +1311,7 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
         return g * (p / den);
       });
   PH_ADD(6, tk2);
-  if ((BSGP_FUSE_COL & 2) && (A.fuse_col & 2)) {  // T == 1: AT's column pass follows here
+  if ((BSGP_FUSE_COL_CODE & 2) && (A.fuse_col & 2)) {  // AT's column pass follows here
     PH_T(tc0);
     team_sync(tm);
     col_conv<COOP>(G, Pt, B.spec, tf_of(G, img, 1), lds);
