@@ -219,6 +219,33 @@ BSGP_HD void stage_generic(const cd* in, cd* out, int n, int R, int Ns, const cd
   const int nb = n / R;
   const int twstep = n / (Ns * R);
   const int rstep = n / R;  // tw[m*rstep] = exp(-2 pi i m / R)
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (nlanes == 64 && 2 * nb * R <= 64) {
+    // A stage that fills at most half the wave (a 31-point transform: 31
+    // outputs): two lanes per output, one summing the even terms r and one
+    // the odd ones, then their partials added (the same sum in both lanes of
+    // the pair) -- half the serial chain, and the lanes that sat idle work.
+    const int q = lane >> 1, half = lane & 1;
+    const bool act = q < nb * R;
+    const int k = act ? q / nb : 0, j = act ? q - k * nb : 0;
+    const int jm = j % Ns;
+    const int od = (j / Ns) * Ns * R + jm;
+    const int k2 = (2 * k) % R;
+    cd acc = cmk(0.0, 0.0);
+    int m = half ? k : 0;  // (r * k) % R
+    for (int r = half; r < R; r += 2) {
+      cd v = in[j + r * nb];
+      if (Ns > 1 && r > 0) v = cmul(v, tw_at(tw, r * jm * twstep, inv));
+      acc = cadd(acc, cmul(v, tw_at(tw, m * rstep, inv)));
+      m += k2;
+      if (m >= R) m -= R;
+    }
+    acc.x += __shfl_xor(acc.x, 1);
+    acc.y += __shfl_xor(acc.y, 1);
+    if (act && half == 0) out[od + k * Ns] = acc;
+    return;
+  }
+#endif
   for (int q = lane; q < nb * R; q += nlanes) {
     const int k = q / nb, j = q - k * nb;  // neighbouring lanes: neighbouring butterflies
     const int jm = j % Ns;
