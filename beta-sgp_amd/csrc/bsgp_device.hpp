@@ -1720,12 +1720,16 @@ __device__ __forceinline__ double beta_deriv_px(double y, double x, double b) {
 // product and the divisions by the float64 scalars, cast to float32, rounded
 // to float32), the others float64; the seven terms are added left to right,
 // each float32 term widened as it is added.
-__device__ __forceinline__ double beta_deriv_px_f32(double y, double x, double b) {
+// `xb_out` (optional) receives the float32 power x**beta, which the same
+// trial's K = sum(s * x**beta) (float32, numpy's order) needs again.
+__device__ __forceinline__ double beta_deriv_px_f32(double y, double x, double b,
+                                                    float* xb_out = nullptr) {
   const double ly = fast_log(y);
   const double yb1 = fast_exp((b - 1) * ly);
   const double yb = fast_exp(b * ly);
   const float xf = (float)x;
   const float xb = (float)pow((double)xf, (double)(float)b);  // x**beta (float32)
+  if (xb_out) *xb_out = xb;
   const float lx = (float)log((double)xf);                      // np.log(x) (float32)
   const float c3 = (float)(b * (b - 1));
   const float c4 = (float)(b * ((b - 1) * (b - 1)));

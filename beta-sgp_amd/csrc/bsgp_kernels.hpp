@@ -1044,19 +1044,26 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
   // float32 (beta_deriv_px_f32).  pw is free scratch until the accept
   // rewrites it (no series moments with adaptive beta).
   const bool k32 = ADAPT && P.gn_f32 != 0;
+  // One-workgroup images keep each trial's float32 powers x**beta from the
+  // beta derivative's pass (xbc, the upper half of pw: the np_f32_sum values
+  // take its first nleaf + nnode floats) for that trial's K, read back after
+  // the pass's block barrier: one float64 pow per pixel and trial less, the
+  // same bits.  Teams recompute them (no data barrier between the pass and K).
+  float* const xbc = (k32 && tm.T == 1) ? reinterpret_cast<float*>(B.pw) + N : nullptr;
   auto konst32 = [&](double b) -> double {
     const float sf = (float)(1 / (b * (b - 1)));
     const double bf = (double)(float)b;  // x**beta: the exponent is cast to float32
     return (double)np_f32_sum(
         A.pw,
         [&](int i) {
+          if (xbc) return sf * xbc[i];
           const double g = g32 ? gdec1(reinterpret_cast<const float*>(B.gns)[i]) : B.gns[i];
           return sf * (float)pow(g, bf);
         },
         reinterpret_cast<float*>(B.pw), Pt, tm);
   };
-  auto bderiv = [&](double den, double g, double b) __attribute__((always_inline)) {
-    return k32 ? beta_deriv_px_f32(den, g, b) : beta_deriv_px(den, g, b);
+  auto bderiv = [&](double den, double g, double b, int i) __attribute__((always_inline)) {
+    return k32 ? beta_deriv_px_f32(den, g, b, xbc ? xbc + i : nullptr) : beta_deriv_px(den, g, b);
   };
   // Small-step series (general beta, fixed beta): with den_i(lam) =
   // a_i (1 + lam u_i), a_i = x_tf_i + bkg_i, u_i = d_tf_i / a_i,
@@ -1103,7 +1110,7 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
       obj.template terms_m<MODE>(xt, xt + bkv, g, &t1[0]);
       if constexpr (adapt) {
         if (!k32) t1[2] += obj.konst(g);
-        t1[3] += bderiv(xt + bkv, g, obj.beta);
+        t1[3] += bderiv(xt + bkv, g, obj.beta, i);
       }
       if (series) {
         const double a = x0 + bkv;
@@ -1199,7 +1206,7 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
     double t[NT];
 #pragma unroll
     for (int k = 0; k < NT; ++k) t[k] = 0.0;
-    auto eval_px = [&](double x0, double dt, double g, double bkv) __attribute__((always_inline)) {
+    auto eval_px = [&](double x0, double dt, double g, double bkv, int i) __attribute__((always_inline)) {
       if constexpr (adapt) {
         if (!k32) t[2 * K] += obj.konst(g);
       }
@@ -1210,7 +1217,7 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
         obj.template terms_m<MODE>(xt, den, g, &t[2 * k]);
       }
       if constexpr (K == 1 && adapt)
-        t[2 * K + 1] += bderiv(x0 + lamk[0] * dt + bkv, g, obj.beta);
+        t[2 * K + 1] += bderiv(x0 + lamk[0] * dt + bkv, g, obj.beta, i);
     };
     const V* xtf = B.xtf;
     const V* dtf = B.dtf;
@@ -1235,8 +1242,8 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
             g0 = gdec1(__int_as_float((int)(w & 0xffffffffLL)));
             g1 = gdec1(__int_as_float((int)(w >> 32)));
           }
-          eval_px(v.x.x, v.d.x, g0, v.b.x);
-          if (!odd || 2 * p + 1 < N) eval_px(v.x.y, v.d.y, g1, v.b.y);
+          eval_px(v.x.x, v.d.x, g0, v.b.x, 2 * p);
+          if (!odd || 2 * p + 1 < N) eval_px(v.x.y, v.d.y, g1, v.b.y, 2 * p + 1);
         });
     team_sum<NT>(t, red, tm);
     if (adapt) konst = k32 ? konst32(obj.beta) : t[2 * K];
