@@ -728,7 +728,11 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   // more workgroups than the team has (C4: 1025 columns, 256-member team)
   a.Tc = T;
   if (T > 1) {
-    const int nc = (p->g.Qh + p->g.nfc - 1) / p->g.nfc;
+    // (one-group cooperative columns pair column 0 with the Nyquist column)
+    const int ncol = (p->g.coop && p->g.nfc == 1 && BSGP_COL_PAIR_NYQ && p->g.Q % 2 == 0)
+                         ? p->g.Qh - 1
+                         : p->g.Qh;
+    const int nc = (ncol + p->g.nfc - 1) / p->g.nfc;
     const int want = 4 * p->ncu / B;
     a.Tc = std::max(T, std::min(nc, want));
   }

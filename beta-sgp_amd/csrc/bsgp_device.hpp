@@ -739,12 +739,68 @@ __device__ __forceinline__ void coop_row_inv_fwd_1(const Geo& G, const Part& D, 
   }
 }
 
+// Columns 0 and Q/2 (Q even) of the half spectrum of real rows are real
+// sequences (each row's DC and Nyquist terms), and so are their convolved
+// columns (the transfer functions of a real kernel are Hermitian along p):
+// they share one complex transform pair, z = c0 + i cN in and out, with the
+// two spectra split by Hermitian symmetry before the transfer functions
+// (r2c_split).  C4's 1025 stored columns then make 1024 transforms, two
+// rounds of the column kernel's 512 resident workgroups instead of a third
+// round for one leftover column.
+#ifndef BSGP_COL_PAIR_NYQ
+#define BSGP_COL_PAIR_NYQ 1
+#endif
+__device__ __forceinline__ void coop_col_pair_nyq(const Geo& G, cd* spec, const cd* tf, cd* a,
+                                                  cd* b) {
+  const int t = threadIdx.x;
+  cd* c0 = spec;
+  cd* cN = spec + (size_t)(G.Qh - 1) * G.H;
+  const cd* t0 = tf;
+  const cd* tN = tf + (size_t)(G.Qh - 1) * G.P;
+  for (int p0 = 0; p0 < G.P; p0 += kBlock * kCCH) {
+    double x0[kCCH], xN[kCCH];
+#pragma unroll
+    for (int u = 0; u < kCCH; ++u) {  // clamped, branch-free
+      const int pc = min(p0 + t + kBlock * u, G.H - 1);
+      x0[u] = c0[pc].x;
+      xN[u] = cN[pc].x;
+    }
+#pragma unroll
+    for (int u = 0; u < kCCH; ++u) {
+      const int p = p0 + t + kBlock * u;
+      if (p < G.P) a[p] = p < G.H ? cmk(x0[u], xN[u]) : cmk(0.0, 0.0);
+    }
+  }
+  __syncthreads();
+  cd* Z = fft_wide(a, b, G.fp, false, t, kBlock, BlockSync());
+  cd* o = (Z == a) ? b : a;
+  for (int p = t; p < G.P; p += kBlock) {
+    cd A, B;
+    r2c_split(Z, G.P, p, &A, &B);
+    const cd X = cmul(A, t0[p]), W = cmul(B, tN[p]);
+    o[p] = cmk(X.x - W.y, X.y + W.x);  // X + i W
+  }
+  __syncthreads();
+  cd* Y = fft_wide(o, Z, G.fp, true, t, kBlock, BlockSync());
+  for (int p = t; p < G.H; p += kBlock) {
+    c0[p] = cmk(Y[p].x, 0.0);
+    cN[p] = cmk(Y[p].y, 0.0);
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ void coop_col_conv_1(const Geo& G, const Part& D, cd* spec, const cd* tf,
                                               cd* lds) {
   const int t = threadIdx.x;
   cd* a = lds;
   cd* b = lds + G.lpad;
-  for (int k = D.gw0; k < G.Qh; k += D.gws) {
+  const bool pair = BSGP_COL_PAIR_NYQ && (G.Q % 2) == 0 && G.Qh > 1;
+  const int kend = pair ? G.Qh - 1 : G.Qh;
+  for (int k = D.gw0; k < kend; k += D.gws) {
+    if (pair && k == 0) {
+      coop_col_pair_nyq(G, spec, tf, a, b);
+      continue;
+    }
     cd* col = spec + (size_t)k * G.H;
     const cd* tk = tf + (size_t)k * G.P;
     for (int p0 = 0; p0 < G.P; p0 += kBlock * kCCH) {
