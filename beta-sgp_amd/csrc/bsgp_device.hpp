@@ -1784,9 +1784,9 @@ __device__ __forceinline__ double beta_deriv_px_f32(double y, double x, double b
   const double yb1 = fast_exp((b - 1) * ly);
   const double yb = fast_exp(b * ly);
   const float xf = (float)x;
-  const float xb = (float)pow((double)xf, (double)(float)b);  // x**beta (float32)
+  const float xb = libm_powf(xf, (float)b);  // x**beta (float32)
   if (xb_out) *xb_out = xb;
-  const float lx = (float)log((double)xf);                      // np.log(x) (float32)
+  const float lx = libm_logf(xf);            // np.log(x) (float32)
   const float c3 = (float)(b * (b - 1));
   const float c4 = (float)(b * ((b - 1) * (b - 1)));
   const float c6 = (float)((b * b) * (b - 1));

@@ -536,9 +536,9 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   double konst32 = 0.0;
   if (konst_f32) {
     const float sf = (float)obj.scal;
-    const double bf = (double)(float)obj.beta;  // x**beta: the exponent is cast to float32
+    const float bf = (float)obj.beta;  // x**beta: the exponent is cast to float32
     konst32 = (double)np_f32_sum(
-        A.pw, [&](int i) { return sf * (float)pow(B.gns[i], bf); },
+        A.pw, [&](int i) { return sf * libm_powf((float)B.gns[i], bf); },
         reinterpret_cast<float*>(B.dtf), D, tm);
   }
   double fsum[3] = {0.0, 0.0, 0.0};  // K, T0, T1
@@ -1049,16 +1049,19 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
   // take its first nleaf + nnode floats) for that trial's K, read back after
   // the pass's block barrier: one float64 pow per pixel and trial less, the
   // same bits.  Teams recompute them (no data barrier between the pass and K).
-  float* const xbc = (k32 && tm.T == 1) ? reinterpret_cast<float*>(B.pw) + N : nullptr;
+  // Only float64 storage has room for it: a float32 pw holds vec_stride floats
+  // and the half spectrum follows right after it.
+  float* const xbc =
+      (k32 && tm.T == 1 && sizeof(V) == 8) ? reinterpret_cast<float*>(B.pw) + N : nullptr;
   auto konst32 = [&](double b) -> double {
     const float sf = (float)(1 / (b * (b - 1)));
-    const double bf = (double)(float)b;  // x**beta: the exponent is cast to float32
+    const float bf = (float)b;  // x**beta: the exponent is cast to float32
     return (double)np_f32_sum(
         A.pw,
         [&](int i) {
           if (xbc) return sf * xbc[i];
           const double g = g32 ? gdec1(reinterpret_cast<const float*>(B.gns)[i]) : B.gns[i];
-          return sf * (float)pow(g, bf);
+          return sf * libm_powf((float)g, bf);
         },
         reinterpret_cast<float*>(B.pw), Pt, tm);
   };

@@ -97,26 +97,60 @@ def make_operators(psf, shape, circular):
 
 # ------------------------------------------------------------ beta-divergence
 # Test hook: when True, the float32 terms x**beta and log(x) of a float32 image
-# are the correctly rounded float32 values (computed in float64, rounded once),
-# the device's arithmetic (bsgp_device.hpp beta_deriv_px_f32, bsgp_kernels.hpp
-# konst32), instead of numpy's vectorised float32 power/log, whose results may
-# be 1 ulp off.  False (the default) is the reference's arithmetic.
-CR_F32 = False
+# come from the C library's powf / logf (oracle/f32libm.c): the arithmetic of
+# numpy 1.26 with its SIMD float32 kernels disabled, under which the reference
+# made the ``_libm`` fixtures (tests/golden/make_golden.py), and the device's
+# (bsgp_math.hpp libm_powf / libm_logf).  False (the default) is this numpy's
+# own float32 power/log.
+LIBM_F32 = False
+_LIBM = []
 
 
 def _is_f32(x):
     return isinstance(x, np.ndarray) and x.dtype.kind == "f" and x.dtype.itemsize == 4
 
 
+def libm_lib():
+    """oracle/_build/libf32libm.so (built by __graft_entry__.build(), or here
+    with gcc when missing)."""
+    if not _LIBM:
+        import ctypes
+        import os
+        import subprocess
+        here = os.path.dirname(os.path.abspath(__file__))
+        so = os.path.join(here, "_build", "libf32libm.so")
+        if not os.path.exists(so):
+            os.makedirs(os.path.dirname(so), exist_ok=True)
+            subprocess.run(["gcc", "-O2", "-shared", "-fPIC", os.path.join(here, "f32libm.c"),
+                            "-o", so, "-lm"], check=True)
+        lib = ctypes.CDLL(so)
+        fp = ctypes.POINTER(ctypes.c_float)
+        lib.bsgp_orc_powf.argtypes = [fp, ctypes.c_float, fp, ctypes.c_long]
+        lib.bsgp_orc_logf.argtypes = [fp, fp, ctypes.c_long]
+        _LIBM.append((lib, fp))
+    return _LIBM[0]
+
+
+def _libm_call(name, x, *extra):
+    import ctypes
+    lib, fp = libm_lib()
+    xc = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(xc)
+    getattr(lib, name)(xc.ctypes.data_as(fp), *extra, out.ctypes.data_as(fp),
+                       ctypes.c_long(xc.size))
+    return out.reshape(np.shape(x))
+
+
 def _pow(x, b):
-    if CR_F32 and _is_f32(x):
-        return (x.astype(np.float64) ** float(np.float32(b))).astype(np.float32)
+    if LIBM_F32 and _is_f32(x):
+        import ctypes
+        return _libm_call("bsgp_orc_powf", x, ctypes.c_float(float(np.float32(b))))
     return x ** b
 
 
 def _log(x):
-    if CR_F32 and _is_f32(x):
-        return np.log(x.astype(np.float64)).astype(np.float32)
+    if LIBM_F32 and _is_f32(x):
+        return _libm_call("bsgp_orc_logf", x)
     return np.log(x)
 
 

@@ -1,6 +1,7 @@
 """Host-side unit tests of the device code's shared headers (CPU, no GPU):
 the Stockham FFT core (incl. the composite radix-6/9 stages of the 270-point
-plan) against a long-double DFT, and fast_log / fast_exp against long double."""
+plan) against a long-double DFT, fast_log / fast_exp against long double, and
+the C-library float32 powf / logf emulation bit for bit against this libm."""
 import os
 import subprocess
 
@@ -10,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "beta-sgp_amd", "csrc")
 
 
-@pytest.mark.parametrize("src", ["fft_core_test.cpp", "math_test.cpp"])
+@pytest.mark.parametrize("src", ["fft_core_test.cpp", "math_test.cpp", "libmf_test.cpp"])
 def test_host_cpp(src, tmp_path):
     exe = tmp_path / src.replace(".cpp", "")
     # -ffp-contract=off: the same rounding as the gfx950 build
