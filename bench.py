@@ -265,19 +265,40 @@ def _free_port():
     return port
 
 
-def launch_ranks(n, argv):
+def launch_ranks(n, argv, poll_s=0.2):
     """`--gpus N` without torchrun: start one rank process per GPU (this
-    process has not touched a GPU), wait for all, return the worst exit code.
-    Rank 0 prints the JSON line."""
+    process has not touched a GPU) and poll them.  As soon as one rank exits
+    non-zero the others are terminated (a rank that died before or after the
+    gloo rendezvous would otherwise leave its peers blocked until the
+    rendezvous / collective timeout) and its exit code is returned; 0 when
+    every rank succeeded.  Rank 0 prints the JSON line."""
     port = _free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0:
+                for q in live:
+                    q.terminate()
+                for q in live:
+                    try:
+                        q.wait(timeout=10)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                print(f"bench: rank {procs.index(p)} exited with {rc}; stopped the other ranks",
+                      file=sys.stderr, flush=True)
+                return rc
+        time.sleep(poll_s)
+    return 0
 
 
 def kernel_bytes(H, W, P, Qh, counters, iters, beta, series, compact, bmap, fused_at_col,
@@ -355,6 +376,9 @@ def parse_args(argv=None):
     ap.add_argument("--stub", action="store_true",
                     help="harness only, no GPU: a fixed CPU wait stands in for each solve "
                          "(tests of the multi-rank path)")
+    ap.add_argument("--stub-fail-rank", type=int, default=None,
+                    help="with --stub: this rank exits 1 before the rendezvous (test of the "
+                         "fail-fast launcher)")
     return ap.parse_args(argv)
 
 
@@ -375,11 +399,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stub and args.stub_fail_rank == rank:
+        sys.exit(1)
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import datetime
+        # a peer that never arrives (or dies mid-run) fails the rendezvous or
+        # the harness's collectives after this long instead of gloo's 30 min
+        tmo = float(os.environ.get("BSGP_DIST_TIMEOUT_S", "300"))
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=tmo))
 
     cfg = CONFIGS[args.config]
     n, k, nstars, circ = cfg["n"], cfg["k"], cfg["nstars"], cfg["circular"]

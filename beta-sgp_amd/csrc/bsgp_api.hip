@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -749,6 +750,10 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   a.pw = p->pw;
   a.storage = p->storage;
   a.spec_off = p->spec_off;
+  {
+    const char* sl = getenv("BSGP_SPIN_LIMIT");
+    a.spin_limit = sl ? (unsigned)strtoul(sl, nullptr, 10) : (1u << 26);
+  }
   a.ls_cap = (prm->beta > 0.0 && prm->beta < 1.0)
                  ? (int)std::ceil(std::log(1e-12) / std::log(prm->beta)) + 2
                  : 4096;

@@ -86,6 +86,8 @@ struct SolveArgs {
   size_t spec_off;      // doubles from a slot's start to its spectrum
   int ls_cap;           // line-search trial cap: lam = beta^(k-1) < 1e-12 ends the search
                         // (sgp.py:336) by trial ceil(log 1e-12 / log beta) + 1 for 0 < beta < 1
+  unsigned spin_limit;  // persistent solver: s_sleep polls before a hand-off wait gives up
+                        // (status bit 4); 2^26 unless BSGP_SPIN_LIMIT says otherwise (tests)
 };
 
 hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s);

@@ -1653,7 +1653,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs 
                 0)
               break;  // every image has stopped: position h is never written
             if (__hip_atomic_load((gi32*)A.tfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
-                spins > (1u << 26)) {
+                spins > A.spin_limit) {
               __hip_atomic_store((gi32*)A.tfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               break;
             }
@@ -1681,9 +1681,9 @@ __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs 
           while (d < need) {
             __builtin_amdgcn_s_sleep(2);
             d = ld_sc1_u32(done + img);
-            if ((++spins & 1023u) == 0 &&
+            if (((++spins & 1023u) == 0 || spins > A.spin_limit) &&
                 (__hip_atomic_load((gi32*)A.tfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
-                 spins > (1u << 26))) {
+                 spins > A.spin_limit)) {
               __hip_atomic_store((gi32*)A.tfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               img = -1;
               break;
@@ -1747,6 +1747,31 @@ __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs 
   }
 }
 
+// After the persistent solver: an image a timed-out hand-off wait abandoned
+// (status bit 4, the tfail word) never reached its stop, so nothing wrote its
+// outputs.  Its completed iterations are reported as if it had stopped there
+// -- x the current iterate, iters, final beta, the counters with bit 4 -- so
+// the host sees the timeout (the phase-kernel path runs such images to MAXIT
+// and reports the same bit).  One workgroup per image; stopped images return.
+template <class V>
+__global__ void __launch_bounds__(kBlock) k_persist_finalize(SolveArgs A) {
+  const int img = A.img0 + (int)blockIdx.x;
+  ImgState& st = A.st[img];
+  if (st.stop) return;
+  const int N = A.g.H * A.g.W;
+  const Bufs<V> B = slot_bufs<V>(A, img, st.par);
+  double* xo = A.out.x + (size_t)img * N;
+  for (int i = threadIdx.x; i < N; i += kBlock) xo[i] = (double)B.xa[i] * st.sc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    st.status |= 4;
+    st.stop = 1;
+    A.out.iters[img] = st.iter - 1;
+    if (A.out.beta_final) A.out.beta_final[img] = st.beta;
+    write_counters(A, st, img, 1);
+  }
+}
+
 // The persistent kernel for a trial width / objective mode (the same choice as
 // ls_kernel); nullptr where no persistent build exists (the phase kernels run).
 template <class V>
@@ -1778,7 +1803,11 @@ inline hipError_t launch_persist_t(const SolveArgs& a, int K, size_t lds, hipStr
   const int mode = P.variant == BSGP_VARIANT_KL ? 0 : special ? -1 : P.gn_f32 ? 4 : 3;
   SolveArgs aa = a;
   void* args[] = {&aa, &queue, &done};
-  return hipLaunchKernel(persist_kernel<V>(K, mode, adapt), dim3(grid), dim3(kBlock), args, lds, s);
+  hipError_t e =
+      hipLaunchKernel(persist_kernel<V>(K, mode, adapt), dim3(grid), dim3(kBlock), args, lds, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_persist_finalize<V>, dim3(a.nimg), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
 }
 
 // ---------------------------------------- kernel: per-iteration tracking

@@ -380,27 +380,32 @@ def _run(variant, gn, psf, bkg, init_recon, proj_type, stop_criterion, MAXIT, ga
         out = plan.solve(gd, bd, prm, flux=fd, x0=xd, obj=od, beta0=b0, want_iterates=bool(save))
     _B.torch.cuda.current_stream().synchronize()
     _B.check_status(out["counters"])
+    def log_run(i, discr):
+        if verbose or stop_criterion in (1, 2, 3, 4):
+            tol = tol_convergence
+            if stop_criterion == 4:  # sgp.py:644, in the image's dtype
+                tol = 1 + 1 / float(np.mean(gn if f32 else np.asarray(gn, dtype=np.float64)))
+            if stop_criterion == 2 and verbose:
+                tol = tol * tol
+            _write_log(stop_criterion, verbose, discr, out["crit"][i].cpu().numpy(),
+                       out["flags"][i].cpu().numpy(), MAXIT, tol)
+
     if betas is not None:
         res = []
         for i in range(len(betas)):
             it = int(out["iters"][i])
-            res.append((out["x"][i].cpu().numpy().reshape(_shape), it,
-                        out["discr"][i, :it + 1].cpu().numpy(),
+            discr = out["discr"][i, :it + 1].cpu().numpy()
+            log_run(i, discr)  # each candidate is one sgp_betaDiv call in the application
+            res.append((out["x"][i].cpu().numpy().reshape(_shape), it, discr,
                         out["times"][i, :it + 1].cpu().numpy(),
                         {"beta": float(out["beta_final"][i]),
-                         "counters": out["counters"][i].cpu().numpy(), "err": None}))
+                         "counters": out["counters"][i].cpu().numpy(), "err": None,
+                         "log": lambda i=i, d=discr: log_run(i, d)}))
         return res
     it = int(out["iters"][0])
     discr = out["discr"][0, :it + 1].cpu().numpy()
     times = out["times"][0, :it + 1].cpu().numpy()
-    if verbose or stop_criterion in (1, 2, 3, 4):
-        tol = tol_convergence
-        if stop_criterion == 4:  # sgp.py:644, in the image's dtype
-            tol = 1 + 1 / float(np.mean(gn if f32 else np.asarray(gn, dtype=np.float64)))
-        if stop_criterion == 2 and verbose:
-            tol = tol * tol
-        _write_log(stop_criterion, verbose, discr, out["crit"][0].cpu().numpy(),
-                   out["flags"][0].cpu().numpy(), MAXIT, tol)
+    log_run(0, discr)
     if save:
         _save_iterates(out["x_iter"][0, :it].cpu().numpy(), gs, _shape)
     x = out["x"][0].cpu().numpy().reshape(_shape)
@@ -708,8 +713,8 @@ def sgp_betaDiv_multistart(gn, psf, bkg, betas=None, score=None, final_solve=Tru
     The application then solves the image once more with the best initial
     beta (:100-107).  The reference is deterministic, so that run repeats the
     best candidate's run exactly; here the candidate's result is returned
-    instead of solving again (with final_solve=True the final run's two
-    printed lines, sgp.py:892-893, are repeated for it).
+    instead of solving again (with final_solve=True the final run's sgp.log
+    lines and its two printed lines, sgp.py:892-893, are repeated for it).
 
     ``score`` is the application's criterion, the photometric flux fractional
     difference 1 - sum(segment_flux(x)) / sum(segment_flux(gn)) (:92-99); it
@@ -764,6 +769,9 @@ def sgp_betaDiv_multistart(gn, psf, bkg, betas=None, score=None, final_solve=Tru
     info = {"betas": betas, "scores": scores, "best_beta": betas[best], "best": best,
             "beta_final": [r[4]["beta"] for r in runs], "candidates": cands}
     if final_solve:
+        # the application's final sgp_betaDiv call repeats the best candidate's
+        # run: its sgp.log lines (sgp.py:748-882) and its two prints (:892-893)
+        runs[best][4]["log"]()
         print(f'Beta parameter in beta-divergence (final value): {runs[best][4]["beta"]}')
         print(f'No. of iterations: {cands[best][1]}')
     return cands[best], info

@@ -104,6 +104,23 @@ def coadd_tiles(tiles, boxes, shape):
     return mean, foot
 
 
+def _check_bkg_dtype(gn_f32, bkg):
+    """A float32 field keeps the reference's float32 arithmetic, where numpy
+    also computes the background's share (bkg scaling, sgp.py:648-666) in the
+    background's own dtype: tiles cut from a float32 / integer background would
+    reach the solve already widened to float64 and silently lose that parity,
+    so they raise here as sgp_betaDiv_batch raises for such backgrounds."""
+    torch = _B.torch
+    if not gn_f32:
+        return
+    dt = bkg.dtype if torch.is_tensor(bkg) else np.asarray(bkg).dtype
+    f64 = dt == torch.float64 if torch.is_tensor(bkg) else (dt.kind == "f" and dt.itemsize == 8)
+    if not f64:
+        raise ValueError("float32 images in a batch need float64 backgrounds (numpy computes the "
+                         "background's part in float32 from a float32 background; solve such "
+                         "images one at a time with sgp_betaDiv / sgp)")
+
+
 def sgp_subdivisions(image, psf, bkg, subdiv_shape=(256, 256), overlap=32, betaParams=None,
                      device_out=False, **sgp_kwargs):
     """Field -> overlapping subdivisions -> one batched beta-SGP solve -> mean
@@ -121,6 +138,7 @@ def sgp_subdivisions(image, psf, bkg, subdiv_shape=(256, 256), overlap=32, betaP
     f32 = (image.dtype == torch.float32) if torch.is_tensor(image) else \
         (np.asarray(image).dtype.kind == "f" and np.asarray(image).dtype.itemsize == 4)
     sgp_kwargs.setdefault("gn_f32", bool(f32))
+    _check_bkg_dtype(sgp_kwargs["gn_f32"], bkg)
     img = _field(image)
     H, W = img.shape
     boxes = subdivision_boxes((H, W), subdiv_shape, overlap)
@@ -170,6 +188,7 @@ def sgp_subdivisions_multistart(image, psf, bkg, betas=None, score=None, subdiv_
     f32 = (image.dtype == torch.float32) if torch.is_tensor(image) else \
         (np.asarray(image).dtype.kind == "f" and np.asarray(image).dtype.itemsize == 4)
     sgp_kwargs.setdefault("gn_f32", bool(f32))
+    _check_bkg_dtype(sgp_kwargs["gn_f32"], bkg)
     img = _field(image)
     H, W = img.shape
     boxes = subdivision_boxes((H, W), subdiv_shape, overlap)

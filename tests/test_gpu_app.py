@@ -86,7 +86,7 @@ def test_float32_arithmetic_is_what_the_reference_does(sgpmod):
     np.testing.assert_allclose(d32, fx["discr"], rtol=1e-7)
 
 
-def test_multistart_candidates_match_reference(sgpmod):
+def test_multistart_candidates_match_reference(sgpmod, tmp_path, monkeypatch):
     """The five seeds of application_sgp_subdivisions.py:70-76 in one batched
     launch: every candidate against its own reference run; then the argmin of
     the caller's score and the final solve with the best initial beta."""
@@ -100,7 +100,16 @@ def test_multistart_candidates_match_reference(sgpmod):
     def score(x):  # stands in for the photometric score; any function of the image
         return -float(np.max(x))
 
+    monkeypatch.chdir(tmp_path)
     final, info = sgpmod.sgp_betaDiv_multistart(gn, psf, bkg, betas=None, score=score, **kw)
+    # sgp.log: every candidate's lines (one sgp_betaDiv call each in the
+    # application) and the final call's, which repeats the best candidate's
+    import logging
+    for h in logging.getLogger().handlers:
+        h.flush()
+    lines = [l for l in open("sgp.log").read().splitlines() if l.startswith("INFO:root:it ")]
+    its = [c[1] for c in info["candidates"]]
+    assert len(lines) == sum(i + 1 for i in its) + its[info["best"]] + 1
     assert info["betas"] == betas
     for i, (x, it, discr, times, none) in enumerate(info["candidates"]):
         fx = target[i]

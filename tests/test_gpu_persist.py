@@ -82,3 +82,29 @@ def test_persistent_more_images_than_slots(sgpmod):
               ccd_sat_level=65000.0, use_original_SGP_Afunction=False, schedule_lr=True,
               adapt_beta=False, betaParams=1.05, team=1)
     both(sgpmod.sgp_betaDiv_batch, gns, fx["psf"], 100.0, **kw)
+
+
+@pytest.mark.parametrize("stop", [1, 3])
+def test_persistent_handoff_timeout_reports_status(sgpmod, monkeypatch, stop):
+    """A hand-off wait that gives up (BSGP_SPIN_LIMIT=0: the first poll that
+    finds the predecessor iteration unfinished) ends the persistent solve
+    with status bit 4 on the images it abandoned (k_persist_finalize), so the
+    drop-in raises instead of returning unwritten outputs; the next solve
+    (default limit) is bitwise the phase kernels again."""
+    import _bsgp
+    fx = golden("ref_lin64_beta.npz")
+    gn = fx["gn"].astype(np.float64)
+    gns = np.stack([np.roll(gn, 3 * i, 0) for i in range(8)])
+    kw = dict(init_recon=2, proj_type=1, stop_criterion=stop, MAXIT=60, tol_convergence=1e-9,
+              alpha=10.0, ccd_sat_level=65000.0, use_original_SGP_Afunction=False,
+              schedule_lr=True, betaParams=1.05, team=1)
+    monkeypatch.setenv("BSGP_SPIN_LIMIT", "0")
+    with pytest.raises(_bsgp.BsgpError, match="timed out"):
+        sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, persistent=1, **kw)
+    out = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, persistent=1, device_out=True, **kw)
+    st = out["counters"].cpu().numpy()[:, 3]
+    it = out["iters"].cpu().numpy()
+    assert np.any(st & 4)
+    assert np.all(it[(st & 4) != 0] < 60) and np.all(it >= 0)
+    monkeypatch.delenv("BSGP_SPIN_LIMIT")
+    both(sgpmod.sgp_betaDiv_batch, gns, fx["psf"], 100.0, **kw)

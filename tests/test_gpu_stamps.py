@@ -32,14 +32,17 @@ from conftest import SVML, konst_ulp_discr, stamp_case, stamp_exact, stamp_oracl
 
 pytestmark = pytest.mark.gpu
 
-# (star, seed) -> cause, for runs allowed to part from the "_libm" reference.
-# The device's float64 FFT and sums differ from pocketfft's and numpy's in the
-# last bits; in the stagnating end of a run that can flip one Armijo test.
+# (star, seed) -> cause, for runs allowed to part from the "_libm" reference:
+# none.  All 40 take the reference's iteration and trial counts in every
+# iteration (measured: x within 1e-5, final beta within 1e-9).
 PARTED_LIBM = {}
-# (star, seed) -> cause, for runs allowed to part from the oracle (numpy 2.2,
-# another pocketfft: the oracle itself parts from the reference in (0, 4) at
-# iteration 33 of 34; under numpy 1.26 it parts nowhere).
-PARTED_ORACLE = {}
+# (star, seed) -> cause, for runs allowed to part from the oracle.
+PARTED_ORACLE = {
+    (0, 4): "the oracle's own parting from the reference: under numpy 2.2 its pocketfft and "
+            "sums round differently from numpy 1.26's in the last bits, which flips the "
+            "stagnating Armijo test of iteration 33 of 34 (test_oracle.py); the device follows "
+            "the reference there",
+}
 
 
 @pytest.fixture(scope="module")

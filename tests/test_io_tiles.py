@@ -186,3 +186,18 @@ def test_subdivision_chain_with_spatial_psf_model():
     m_ref, c_ref = tiles_oracle.coadd_mean(ref, boxes, gn.shape)
     np.testing.assert_array_equal(foot, c_ref)
     assert np.linalg.norm(mosaic - m_ref) / np.linalg.norm(m_ref) < 1e-5
+
+
+def test_float32_field_needs_float64_background():
+    """A float32 field with a float32 (or integer) background map raises
+    before any tile is cut (the background's float32 share of the prelude
+    would otherwise be lost in the float64 tiles); float64 maps and Python /
+    float64 scalars pass (host-side guard, no GPU)."""
+    import subdivisions
+    with pytest.raises(ValueError, match="float64 backgrounds"):
+        subdivisions._check_bkg_dtype(True, np.ones((8, 8), np.float32))
+    with pytest.raises(ValueError, match="float64 backgrounds"):
+        subdivisions._check_bkg_dtype(True, np.int32(3))
+    subdivisions._check_bkg_dtype(True, np.ones((8, 8)))
+    subdivisions._check_bkg_dtype(True, 100.0)
+    subdivisions._check_bkg_dtype(False, np.ones((8, 8), np.float32))

@@ -81,3 +81,26 @@ def test_shard_bounds_cover_the_job():
         parts = [bench.shard_bounds(8192, world, r) for r in range(world)]
         assert parts[0][0] == 0 and parts[-1][1] == 8192
         assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
+
+
+@pytest.mark.parametrize("fail_rank", [0, 1])
+def test_bench_fails_fast_when_a_rank_dies(fail_rank):
+    """One rank exits 1 before the gloo rendezvous: the launcher stops the
+    other rank (which would otherwise wait in the rendezvous until its
+    timeout) and returns non-zero within seconds."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    t0 = time.time()
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--stub",
+                          "--stub-fail-rank", str(fail_rank), "--steps", "3", "--warmup", "1",
+                          "--no-cpu", "--config", "c3", "--maxit", "10"], capture_output=True,
+                         text=True, timeout=120, env=env)
+    el = time.time() - t0
+    assert out.returncode != 0
+    assert el < 30, el
+    assert f"rank {fail_rank} exited with 1" in out.stderr
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
