@@ -87,6 +87,12 @@ CONFIGS = {
     # cuts 375x375 tiles): a 400-point grid, cooperative transforms
     "sub375": dict(n=375, k=31, nstars=300, batch=512, circular=False,
                    desc="{B} independent {n}x{n} subdivision-size tiles, 31x31 PSF, linear A"),
+    # the application's CROWDED mode solves its whole 450x450 frame
+    # (application_sgp_subdivisions.py:22,44-50): a 480-point grid; published
+    # reference rates 4.98 beta-SGP / 3.50 KL it/s for one frame
+    # (results/CROWDED_SUBDIV_EXEC_TIME*.npy, NUM_ITERS*.npy; hardware unstated)
+    "sub450": dict(n=450, k=31, nstars=400, batch=512, circular=False,
+                   desc="{B} independent {n}x{n} CROWDED-frame-size tiles, 31x31 PSF, linear A"),
     # application_sgp_star_stamps.py:56-105: 31x31 float32 cutouts around stars,
     # the DIAPL PSF with the default circular A, adaptive beta, stop rule 3, the
     # five seeds; the reference's only first-party throughput figure

@@ -365,6 +365,18 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   p->wg_per_cu = 4;
   auto need = [&](int n) { return (size_t)n * 2 * g.lpad * sizeof(cd) + red_bytes; };
   g.coop = 0;
+  // per-wave transforms at three workgroups per CU (12 waves/CU) before the
+  // cooperative build's one 512-thread workgroup per CU (8 waves): 375^2 tiles
+  // on their 400-point grid fit (52.9 KB of 54.3 KB)
+  {
+    const char* e = getenv("BSGP_PERWAVE_MIN_WG");
+    const int min_wg = e ? atoi(e) : BSGP_PERWAVE_MIN_WG;
+    const size_t b3 = 160 * 1024 / 3 - 256;
+    if (min_wg <= 3 && need(kWaves) > budget && need(kWaves) <= b3) {
+      budget = b3;
+      p->wg_per_cu = 3;
+    }
+  }
   if (need(kWaves) > budget) {
     // transforms too long for a wave each at four workgroups per CU: the
     // whole workgroup runs one transform at a time (cooperative passes)
@@ -779,9 +791,11 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   // after setup and after every iteration, off the hot kernels
   const bool track = out->err != nullptr || out->x_iter != nullptr;
   // persistent solver (one launch for every iteration, k_persist): one-workgroup
-  // images with per-wave transforms; it overlaps the phases of different images
-  // itself, so it runs the whole batch as one sub-batch
-  const bool persist = prm->persistent && T == 1 && !p->g.coop && !track;
+  // images, with per-wave transforms or (cooperative plans: the application's
+  // 375^2 / 450^2 subdivisions) the 512-thread build's thread-group transforms
+  // (bsgp_persist_c512.hip); it overlaps the phases of different images itself,
+  // so it runs the whole batch as one sub-batch
+  const bool persist = prm->persistent && T == 1 && (!p->g.coop || BSGP_COOP512) && !track;
   if (persist) S = 1;
   // sub-batch 0 runs on the caller's stream itself, sub-batches 1..S-1 on the
   // plan's streams: S streams in all, so S = 4 fits the 4 hardware queues HIP

@@ -144,6 +144,12 @@ void persist_kernels_all(std::vector<const void*>& f);
 // cooperative plans: at most this many thread groups per workgroup run
 // transforms side by side (bsgp_device.hpp coop passes), and the column
 // kernel's groups (0: the same as the other kernels)
+// plans whose per-wave transforms fit the LDS at three workgroups per CU (but
+// not four) take them instead of the cooperative build when this is <= 3
+// (runtime override: BSGP_PERWAVE_MIN_WG)
+#ifndef BSGP_PERWAVE_MIN_WG
+#define BSGP_PERWAVE_MIN_WG 4
+#endif
 #ifndef BSGP_COOP_GROUPS
 #define BSGP_COOP_GROUPS 4
 #endif
@@ -170,5 +176,10 @@ hipError_t bsgp_c512_launch_iteration(const void* a, int K, size_t lds, hipStrea
                                       hipEvent_t* ev);
 hipError_t bsgp_c512_team_resident(int storage, size_t lds, int* per_cu);
 hipError_t bsgp_c512_set_lds_limit(size_t bytes);
+// the cooperative plans' persistent solver (bsgp_persist_c512.hip)
+hipError_t bsgp_c512_launch_persist(const void* a, int K, size_t lds, hipStream_t s,
+                                    unsigned* queue, unsigned* done, int grid);
+hipError_t bsgp_c512_persist_resident(const void* a, int K, size_t lds, int* per_cu);
+hipError_t bsgp_c512_persist_set_lds_limit(size_t bytes);
 hipError_t bsgp_c512_phase_prof(unsigned long long* out, int n, int reset);
 }

@@ -1544,7 +1544,13 @@ static __global__ void k_ring_init(unsigned* queue, int nimg, int img0) {
 }
 
 #ifndef BSGP_PERSIST_ATTR
-#define BSGP_PERSIST_ATTR __attribute__((amdgpu_waves_per_eu(3)))
+// (per-wave plans: 3 waves/SIMD, the phase kernels' own; cooperative plans'
+// 512-thread workgroups: 2 waves/SIMD per workgroup, BSGP_PERSIST_COOP_WAVES)
+#ifndef BSGP_PERSIST_COOP_WAVES
+#define BSGP_PERSIST_COOP_WAVES 2
+#endif
+#define BSGP_PERSIST_ATTR \
+  __attribute__((amdgpu_waves_per_eu(COOP ? BSGP_PERSIST_COOP_WAVES : 3)))
 #endif
 
 __device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long long* p) {
@@ -1586,10 +1592,11 @@ __device__ __forceinline__ const SolveArgs& args_of(ArgRef r) {
   asm volatile("" : "+s"(p));  // re-read per call: nothing of it is hoisted across phases
   return *(const SolveArgs*)p;
 }
-template <class V>
+template <bool COOP, class V>
 __device__ BSGP_PERSIST_FN void persist_dir(ArgRef r, int img) {
-  dir_phase<false, V>(args_of(r), __builtin_amdgcn_readfirstlane(img));
+  dir_phase<COOP, V>(args_of(r), __builtin_amdgcn_readfirstlane(img));
 }
+template <bool COOP>
 __device__ BSGP_PERSIST_FN void persist_col_a(ArgRef r, int img) {
   const SolveArgs& A = args_of(r);
   img = __builtin_amdgcn_readfirstlane(img);
@@ -1599,16 +1606,18 @@ __device__ BSGP_PERSIST_FN void persist_col_a(ArgRef r, int img) {
   tm.T = 1;
   const Bufs<double> Bd = slot_bufs<double>(A, img, 0);  // spec only (same offset for V)
   PH_T(tc0);
-  col_conv<false>(A.g, make_part(tm, A.g.nfw, A.g.W), Bd.spec, tf_of(A.g, img, 0), lds);
+  // (a cooperative plan's column pass on its column groups, as k_col)
+  col_conv<COOP>(A.g, make_part(tm, COOP ? A.g.nfc : A.g.nfw, A.g.W), Bd.spec,
+                 tf_of(A.g, img, 0), lds);
   PH_ADD(3, tc0);
 }
-template <int K, int MODE, bool ADAPT, class V>
+template <int K, int MODE, bool ADAPT, bool COOP, class V>
 __device__ BSGP_PERSIST_FN void persist_ls(ArgRef r, int img) {
-  ls_phase<K, MODE, ADAPT, false, V>(args_of(r), __builtin_amdgcn_readfirstlane(img));
+  ls_phase<K, MODE, ADAPT, COOP, V>(args_of(r), __builtin_amdgcn_readfirstlane(img));
 }
-template <class V>
+template <bool COOP, class V>
 __device__ BSGP_PERSIST_FN void persist_bb(ArgRef r, int img) {
-  bb_phase<false, V>(args_of(r), __builtin_amdgcn_readfirstlane(img));
+  bb_phase<COOP, V>(args_of(r), __builtin_amdgcn_readfirstlane(img));
 }
 
 // Slot order (fixed-length solves, stop rules 0/1): task t = (k - 1) * nimg + i
@@ -1622,7 +1631,7 @@ __device__ __forceinline__ unsigned ld_sc1_u32(const unsigned* p) {
   return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int K, int MODE, bool ADAPT, class V>
+template <bool COOP, int K, int MODE, bool ADAPT, class V>
 __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs A,
                                                                         unsigned* queue,
                                                                         unsigned* done) {
@@ -1716,12 +1725,12 @@ __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs 
     if (img == -1) break;
     if (img < 0) continue;
     const ArgRef ar = kernarg_ref();
-    persist_dir<V>(ar, img);
+    persist_dir<COOP, V>(ar, img);
     __syncthreads();  // rows of d and the direction scalars complete
-    persist_col_a(ar, img);
-    persist_ls<K, MODE, ADAPT, V>(ar, img);
+    persist_col_a<COOP>(ar, img);
+    persist_ls<K, MODE, ADAPT, COOP, V>(ar, img);
     __syncthreads();  // the accepted step and AT's columns complete
-    persist_bb<V>(ar, img);
+    persist_bb<COOP, V>(ar, img);
     // hand the image on: every wave's stores drained, then lane 0 releases at
     // agent scope and publishes (sc1 store): ring append, or done[img]
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1774,24 +1783,25 @@ __global__ void __launch_bounds__(kBlock) k_persist_finalize(SolveArgs A) {
 
 // The persistent kernel for a trial width / objective mode (the same choice as
 // ls_kernel); nullptr where no persistent build exists (the phase kernels run).
-template <class V>
+template <class V, bool COOP = false>
 inline const void* persist_kernel(int K, int mode, bool adapt) {
-  if (adapt) return (const void*)k_persist<1, -1, true, V>;
+  if (adapt) return (const void*)k_persist<COOP, 1, -1, true, V>;
   if (K > 2) K = 2;
-  if (mode == -1) return (const void*)k_persist<2, -1, false, V>;
-  if (mode == 0) return K == 1 ? (const void*)k_persist<1, 0, false, V>
-                               : (const void*)k_persist<2, 0, false, V>;
-  if (mode == 4) return K == 1 ? (const void*)k_persist<1, 4, false, V>
-                               : (const void*)k_persist<2, 4, false, V>;
-  return K == 1 ? (const void*)k_persist<1, 3, false, V> : (const void*)k_persist<2, 3, false, V>;
+  if (mode == -1) return (const void*)k_persist<COOP, 2, -1, false, V>;
+  if (mode == 0) return K == 1 ? (const void*)k_persist<COOP, 1, 0, false, V>
+                               : (const void*)k_persist<COOP, 2, 0, false, V>;
+  if (mode == 4) return K == 1 ? (const void*)k_persist<COOP, 1, 4, false, V>
+                               : (const void*)k_persist<COOP, 2, 4, false, V>;
+  return K == 1 ? (const void*)k_persist<COOP, 1, 3, false, V>
+                : (const void*)k_persist<COOP, 2, 3, false, V>;
 }
-template <class V>
+template <class V, bool COOP = false>
 inline void persist_kernels(std::vector<const void*>& f) {
   for (int adapt = 0; adapt < 2; ++adapt)
     for (int mode : {-1, 0, 3, 4})
-      for (int K : {1, 2}) f.push_back(persist_kernel<V>(K, mode, adapt != 0));
+      for (int K : {1, 2}) f.push_back(persist_kernel<V, COOP>(K, mode, adapt != 0));
 }
-template <class V>
+template <class V, bool COOP = false>
 inline hipError_t launch_persist_t(const SolveArgs& a, int K, size_t lds, hipStream_t s,
                                    unsigned* queue, unsigned* done, int grid) {
   if (a.prm.stop_criterion >= 2 && a.prm.stop_criterion <= 4)
@@ -1803,8 +1813,8 @@ inline hipError_t launch_persist_t(const SolveArgs& a, int K, size_t lds, hipStr
   const int mode = P.variant == BSGP_VARIANT_KL ? 0 : special ? -1 : P.gn_f32 ? 4 : 3;
   SolveArgs aa = a;
   void* args[] = {&aa, &queue, &done};
-  hipError_t e =
-      hipLaunchKernel(persist_kernel<V>(K, mode, adapt), dim3(grid), dim3(kBlock), args, lds, s);
+  hipError_t e = hipLaunchKernel(persist_kernel<V, COOP>(K, mode, adapt), dim3(grid),
+                                 dim3(kBlock), args, lds, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_persist_finalize<V>, dim3(a.nimg), dim3(kBlock), 0, s, a);
   return hipGetLastError();

@@ -98,6 +98,28 @@ def app_case(name, variant=LIBM):
     return gn, sub["psf"], bkg, kw, str(fx["fn"]), fx
 
 
+def crowded_case(name, variant=LIBM):
+    """The application's CROWDED mode (make_golden.py crowded): the whole
+    450x450 float32 frame results/CROWDED_SUBDIV_ORIGIMG.fits, its background
+    map, the published flux, the application's kwargs (stop rule 3, tol 1e-5)
+    -- inputs, and the reference's outputs of fixture set `variant`."""
+    fx = golden(f"ref_{name}{variant}.npz")
+    z = golden("crowded_inputs.npz")
+    _, psf = __import__("fits_io").read_fits(os.path.join(GOLDEN, "psfccfbrd210048_1_1_img.fits"))
+    kw = ref_kwargs(fx)
+    kw["flux"] = np.float64(z["flux_beta"] if str(fx["fn"]) == "sgp_betaDiv" else z["flux_kl"])
+    return z["img"], psf, z["bkg"], kw, str(fx["fn"]), fx
+
+
+def satellite_case(name):
+    """simulation_test_sgp.py's satellite runs (make_golden.py satellite):
+    image, psf, background, ground truth, kwargs, function name, reference
+    outputs (x, discr, rel_err and the FFT-swap spread of rel_err)."""
+    d = golden("satellite_inputs.npz")
+    fx = golden(f"ref_{name}.npz")
+    return (d["gn"], d["psf"], d["bg"][0][0], d["obj"], ref_kwargs(fx), str(fx["fn"]), fx)
+
+
 APP_CASES = ["app_beta0", "app_beta1", "app_beta2", "app_beta3", "app_beta4", "app_kl",
              "app_beta2_flux32", "app_crop_beta"]
 

@@ -658,6 +658,89 @@ def make_app():
         print(f"{name:18s} {fn:12s} iters={it:3d} discr0={discr[0]:.10f} discrN={discr[-1]:.10f}")
 
 
+def make_satellite():
+    """simulation_test_sgp.py:37-56 (KL) and :112-169 (beta = 1.0001, fixed):
+    the satellite image for 332 iterations, circular A, init_recon 3, stop
+    rule 1 (py3.10 / numpy 2.2).  Stores x, discr and the reference's
+    rel_err = sqrt(sum((x - obj)^2) / sum(obj^2)) of each run, and the same
+    runs with numpy's FFT swapped for scipy.fft (only FFT rounding changes):
+    at 332 iterations the trajectories are chaotic, so that
+    variant's rel_err measures how far a faithful restatement with another
+    FFT may land."""
+    import scipy.fft
+    from scipy.io import loadmat
+    sgp, fcp = import_reference(need_astropy=False)
+    sat = loadmat(os.path.join(REF, "simulated_test/data/satellite_25500.mat"))
+    image, psf, bkg, obj = sat["gn"], sat["psf"], sat["bg"][0][0], sat["obj"]
+
+    def relerr(x):
+        e = x - obj
+        return float(np.sqrt(np.sum(e * e) / np.sum(obj * obj)))
+
+    runs = {"sat_kl332": ("sgp", dict(init_recon=3, stop_criterion=1, MAXIT=332)),
+            "sat_beta332": ("sgp_betaDiv", dict(init_recon=3, stop_criterion=1, MAXIT=332,
+                                                betaParam=1.0001, lr=1e-3, lr_exp_param=0.1,
+                                                schedule_lr=True, adapt_beta=False))}
+    for name, (fn, kw) in runs.items():
+        x, it, discr, _, _ = run_quiet(getattr(sgp, fn), image, psf, bkg, **kw)
+        f1, f2 = sgp.np.fft.fftn, sgp.np.fft.ifftn
+        try:
+            sgp.np.fft.fftn, sgp.np.fft.ifftn = scipy.fft.fftn, scipy.fft.ifftn
+            xs, _, discr_s, _, _ = run_quiet(getattr(sgp, fn), image, psf, bkg, **kw)
+        finally:
+            sgp.np.fft.fftn, sgp.np.fft.ifftn = f1, f2
+        np.savez_compressed(os.path.join(OUT, f"ref_{name}.npz"), x=x, iters=it, discr=discr,
+                            relerr=relerr(x), relerr_scipyfft=relerr(xs),
+                            x_rel_scipyfft=float(np.linalg.norm(xs - x) / np.linalg.norm(x)),
+                            kwargs=repr(kw), fn=fn)
+        print(f"{name}: iters={it} relerr={relerr(x):.10f} scipy.fft relerr={relerr(xs):.10f} "
+              f"x rel {np.linalg.norm(xs - x) / np.linalg.norm(x):.2e}")
+
+
+def make_crowded():
+    """The application's CROWDED mode (application_sgp_subdivisions.py:22,
+    44-50, 84-115): the whole 450x450 float32 frame
+    results/CROWDED_SUBDIV_ORIGIMG.fits, no crop, beta-SGP from the published
+    best initial beta (results/CROWDED_SUBDIV_BEST_BETA_INIT.npy) and the KL
+    branch, stop rule 3 at tol 1e-5, the application's kwargs.  The provided
+    flux is the application's orig_scat['segment_flux'].value.sum() from the
+    published per-source fluxes (results/CROWDED_SUBDIV_ORIG_FLUX[_BETA].npy).
+    Stand-ins (the inputs are not in the reference): the crowded frame's own
+    PSF file (psfccfbvc310082_3_3_img.fits) is absent, so the DIAPL PSF of
+    psf/ is used; photutils' Background2D is absent, so the background map is
+    app_background (median-filtered, smoothed frame)."""
+    sgp, fcp = import_reference(need_astropy=True)
+    from astropy.io import fits
+    res = "/root/reference/results"
+    img = fits.getdata(os.path.join(res, "CROWDED_SUBDIV_ORIGIMG.fits"))  # (450, 450) >f4
+    psf = fits.getdata("/root/reference/psf/psfccfbrd210048_1_1_img.fits")  # (31, 31) >f8
+    assert img.shape == (450, 450) and img.dtype == np.dtype(">f4")
+    inp = os.path.join(OUT, "crowded_inputs.npz")
+    if _suffix() == "_libm":  # the committed inputs (numpy's SIMD exp enters the map)
+        z = np.load(inp)
+        assert np.array_equal(z["img"], img)
+        bkg = z["bkg"]
+    else:
+        bkg = app_background(img)
+    flux_b = np.float64(np.load(os.path.join(res, "CROWDED_SUBDIV_ORIG_FLUX_BETA.npy")).sum())
+    flux_k = np.float64(np.load(os.path.join(res, "CROWDED_SUBDIV_ORIG_FLUX.npy")).sum())
+    beta0 = float(np.load(os.path.join(res, "CROWDED_SUBDIV_BEST_BETA_INIT.npy")))
+    if _suffix() != "_libm":
+        np.savez_compressed(inp, img=img, bkg=bkg, flux_beta=np.array(flux_b),
+                            flux_kl=np.array(flux_k), beta0=np.array(beta0))
+    runs = {"crowded_beta": ("sgp_betaDiv", dict(app_kwargs(flux_b), betaParam=beta0, lr=1e-3,
+                                                 lr_exp_param=0.1, schedule_lr=True,
+                                                 adapt_beta=False)),
+            "crowded_kl": ("sgp", app_kwargs(flux_k))}
+    for name, (fn, kw) in runs.items():
+        x, it, discr, _, _ = run_quiet(getattr(sgp, fn), img, psf, bkg, **kw)
+        kws = {k: v for k, v in kw.items() if k != "flux"}
+        np.savez_compressed(os.path.join(OUT, f"ref_{name}{_suffix()}.npz"), x=x, iters=it,
+                            discr=discr, kwargs=repr(kws), fn=fn,
+                            flux_dtype=str(np.asarray(kw["flux"]).dtype))
+        print(f"{name:14s} {fn:12s} iters={it:3d} discr0={discr[0]:.10f} discrN={discr[-1]:.10f}")
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "circular"
     cwd = os.getcwd()
@@ -678,6 +761,10 @@ if __name__ == "__main__":
                 make_c4()
             elif which == "stamps":
                 make_stamps()
+            elif which == "crowded":
+                make_crowded()
+            elif which == "satellite":
+                make_satellite()
             else:
                 make_linear()
         finally:

@@ -60,6 +60,35 @@ def test_application_path_matches_reference(name, sgpmod):
     assert abs(x.sum() - f) <= tol * f
 
 
+def test_crowded_full_frame_matches_reference(sgpmod, monkeypatch):
+    """The application's CROWDED mode (application_sgp_subdivisions.py:22,
+    44-50, 84-115): the whole 450x450 float32 frame on its 480-point grid, a
+    background map, the published flux, beta-SGP from the published best
+    initial beta and the KL branch (stop rule 3, tol 1e-5): the single-image
+    drop-in (automatic team) and a one-workgroup batch of both frames (the
+    cooperative plans' persistent solver) against the reference's runs."""
+    from conftest import crowded_case
+    for name in ("crowded_beta", "crowded_kl"):
+        gn, psf, bkg, kw, fn, fx = crowded_case(name)
+        assert gn.shape == (450, 450) and gn.dtype == np.dtype(">f4")
+        x, it, discr, _, _ = getattr(sgpmod, fn)(gn, psf, bkg, **kw)
+        assert it == int(fx["iters"]), (name, it, int(fx["iters"]))
+        assert rel(x, fx["x"]) < SOLVE_RTOL, (name, rel(x, fx["x"]))
+        np.testing.assert_allclose(discr, fx["discr"], rtol=1e-7)
+        kb = dict(kw)
+        f = kb.pop("flux")
+        if fn == "sgp_betaDiv":
+            b = kb.pop("betaParam")
+            out = sgpmod.sgp_betaDiv_batch(np.stack([gn, gn]), psf, bkg, betaParams=[b, b],
+                                           flux=f, team=1, **kb)
+        else:
+            out = sgpmod.sgp_batch(np.stack([gn, gn]), psf, bkg, flux=f, team=1, **kb)
+        for i in range(2):
+            assert int(out["iters"][i]) == int(fx["iters"])
+            assert rel(out["x"][i], fx["x"]) < SOLVE_RTOL
+            np.testing.assert_allclose(out["discr"][i, :it + 1], fx["discr"], rtol=1e-7)
+
+
 @pytest.mark.parametrize("name", APP_CASES)
 def test_application_path_svml_set(name, sgpmod):
     """The same runs against the reference under numpy's default float32

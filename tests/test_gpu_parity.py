@@ -190,6 +190,28 @@ def test_ngc_kl27_known_answer(sgpmod, ngc):
     assert it == 27 and len(discr) == 28
 
 
+@pytest.mark.parametrize("name", ["sat_kl332", "sat_beta332"])
+def test_satellite_332_known_answer(sgpmod, name):
+    """simulation_test_sgp.py:37-56 / 112-169: the satellite for 332
+    iterations, rel. error vs ground truth 0.2904372552 (KL) and
+    0.2910767378 (beta = 1.0001).  At 332 iterations the runs are chaotic
+    (SURVEY §4): the reference itself with scipy.fft in place of numpy's FFT
+    lands rel_err 2.1e-4 / 3.2e-4 away (recorded in the fixture).  The
+    device's FFT rounds differently again, so its rel_err must lie within 3x
+    that spread of the reference's, and its discrepancy follow the
+    reference's through iteration 50 (before the chaos) at rtol 1e-7."""
+    from conftest import satellite_case
+    gn, psf, bkg, obj, kw, fn, fx = satellite_case(name)
+    x, it, discr, _, _ = getattr(sgpmod, fn)(gn, psf, bkg, **kw)
+    assert it == 332 and len(discr) == 333
+    relerr = float(np.sqrt(np.sum((x - obj) ** 2) / np.sum(obj * obj)))
+    spread = abs(float(fx["relerr_scipyfft"]) - float(fx["relerr"]))
+    print(name, "rel_err", relerr, "reference", float(fx["relerr"]), "spread", spread,
+          "x rel", rel(x, fx["x"]))
+    assert abs(relerr - float(fx["relerr"])) <= 3 * spread, (relerr, spread)
+    np.testing.assert_allclose(discr[:51], fx["discr"][:51], rtol=1e-7)
+
+
 def test_stamp31_odd_size_adaptive_beta(sgpmod):
     fx = golden("ref_stamp31_beta_adapt.npz")
     x, it, discr, _, _ = sgpmod.sgp_betaDiv(fx["gn"], fx["psf"], np.float64(20.0), init_recon=2,

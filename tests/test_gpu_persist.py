@@ -108,3 +108,34 @@ def test_persistent_handoff_timeout_reports_status(sgpmod, monkeypatch, stop):
     assert np.all(it[(st & 4) != 0] < 60) and np.all(it >= 0)
     monkeypatch.delenv("BSGP_SPIN_LIMIT")
     both(sgpmod.sgp_betaDiv_batch, gns, fx["psf"], 100.0, **kw)
+
+
+@pytest.mark.parametrize("case", ["app_f32", "f64", "adapt", "f32storage", "kl"])
+def test_persistent_cooperative_plans_bitwise(sgpmod, case):
+    """Cooperative plans (Geo::coop: the application's 375x375 subdivisions on
+    their 400-point grid, thread-group transforms in 512-thread workgroups)
+    run the persistent solver of bsgp_persist_c512.hip: bitwise the
+    cooperative phase kernels, for the application's float32 FITS tile (its
+    background map, flux, stop rule 3) and float64 images, both storages,
+    adaptive beta and KL."""
+    from conftest import app_case
+    gn, psf, bkg, kw, fn, fx = app_case("app_beta0")
+    kw = dict(kw)
+    b0 = kw.pop("betaParam")
+    flux = kw.pop("flux")
+    kw.pop("adapt_beta", None)
+    g = np.asarray(gn)
+    gns = np.stack([g, np.roll(g, 37, 0), np.roll(g, 11, 1)])
+    if case != "app_f32":
+        gns = gns.astype(np.float64)
+    kw.update(MAXIT=12, team=1)
+    if case == "kl":
+        kw.pop("tol_convergence", None)
+        both(sgpmod.sgp_batch, gns, psf, bkg, flux=flux, **kw)
+        return
+    extra = dict(adapt_beta=case == "adapt", storage="f32" if case == "f32storage" else "f64")
+    out = both(sgpmod.sgp_betaDiv_batch, gns, psf, bkg, flux=flux,
+               betaParams=[b0, 1.02, 0.97], **kw, **extra)
+    if case == "app_f32":  # the first image is the application's run (fixture to 12 iterations)
+        assert int(out["iters"][0]) <= int(fx["iters"])
+        np.testing.assert_allclose(out["discr"][0, :13], fx["discr"][:13], rtol=1e-7)

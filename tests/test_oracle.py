@@ -216,3 +216,23 @@ def test_numpy_f32_sum_model(n):
     for seed in range(3):
         a = np.random.default_rng(1000 * n + seed).uniform(-1, 3, n).astype(np.float32)
         assert _pairwise_model(a, prog, counts) == np.sum(a)
+
+
+@pytest.mark.parametrize("name", ["sat_kl332", "sat_beta332"])
+def test_oracle_satellite_332_iterations(name):
+    """simulation_test_sgp.py:37-56 / 112-169, the reference's satellite
+    runs (332 iterations, KL and fixed beta = 1.0001): the reference's own
+    rel_err 0.2904372552 / 0.2910767378 (SURVEY §4 KATs).  Chaotic at this
+    length: with numpy's FFT swapped for scipy.fft the reference itself moves
+    x by 4.0e-2 / 5.2e-3 and rel_err by 2.1e-4 / 3.2e-4 (the fixture records
+    that variant).  The oracle runs the same numpy as the fixture here and
+    must land within that spread; its first 50 discrepancies match at 1e-7."""
+    from conftest import satellite_case
+    gn, psf, bkg, obj, kw, fn, fx = satellite_case(name)
+    x, it, discr, _, _ = getattr(orc, fn)(gn, psf, bkg, **kw)
+    assert it == 332
+    e = x - obj
+    rel = float(np.sqrt(np.sum(e * e) / np.sum(obj * obj)))
+    spread = abs(float(fx["relerr_scipyfft"]) - float(fx["relerr"]))
+    assert abs(rel - float(fx["relerr"])) <= spread, (rel, float(fx["relerr"]), spread)
+    np.testing.assert_allclose(discr[:51], fx["discr"][:51], rtol=1e-7)
