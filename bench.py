@@ -85,7 +85,9 @@ CONFIGS = {
                     "rank), 25x25 PSF, linear A"),
     # the application's subdivision tiles (application_sgp_subdivisions.py:43-107
     # cuts 375x375 tiles): a 400-point grid, cooperative transforms
-    "sub375": dict(n=375, k=31, nstars=300, batch=512, circular=False,
+    # 1024 tiles: per-wave transforms at three workgroups per CU hold 768
+    # images at once, so a launch of 1024 keeps every slot busy to the end
+    "sub375": dict(n=375, k=31, nstars=300, batch=1024, circular=False,
                    desc="{B} independent {n}x{n} subdivision-size tiles, 31x31 PSF, linear A"),
     # the application's CROWDED mode solves its whole 450x450 frame
     # (application_sgp_subdivisions.py:22,44-50): a 480-point grid; published

@@ -371,10 +371,12 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   {
     const char* e = getenv("BSGP_PERWAVE_MIN_WG");
     const int min_wg = e ? atoi(e) : BSGP_PERWAVE_MIN_WG;
-    const size_t b3 = 160 * 1024 / 3 - 256;
-    if (min_wg <= 3 && need(kWaves) > budget && need(kWaves) <= b3) {
-      budget = b3;
-      p->wg_per_cu = 3;
+    for (int wg = 3; wg >= 2 && wg >= min_wg; --wg) {
+      const size_t bw = 160 * 1024 / wg - 256;
+      if (need(kWaves) > budget && need(kWaves) <= bw) {
+        budget = bw;
+        p->wg_per_cu = wg;
+      }
     }
   }
   if (need(kWaves) > budget) {
@@ -432,6 +434,10 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
                        bsgp_c512_block() != kCoopBlock)) {
     delete p;
     return fail(BSGP_ERR_HIP, "cooperative 512-thread build does not match this library");
+  }
+  if (bsgp_app_args_size() != sizeof(SolveArgs)) {
+    delete p;
+    return fail(BSGP_ERR_HIP, "application-size persistent build does not match this library");
   }
   if (set_solver_lds_limit(p->lds_bytes) != hipSuccess) {
     delete p;

@@ -56,8 +56,17 @@ struct FftPlan {
 };
 
 // Lengths with a compile-time transform (the hot grid sizes: 256 for circular
-// 256^2 images, 270 for 256^2 images with a 25x25 PSF in linear mode).
-BSGP_HD bool fft_static_len(int n) { return n == 256 || n == 270; }
+// 256^2 images, 270 for 256^2 images with a 25x25 PSF in linear mode, and
+// in builds with BSGP_FFT_STATIC_APP -- the persistent solver of
+// bsgp_persist_app.hip -- the application's 375^2 / 450^2 subdivisions with
+// the 31x31 DIAPL PSF in linear mode: 400 and 480).  Only that build inlines
+// them: in every kernel the extra straight-line stages cost C3 0.7 % (A/B).
+#ifndef BSGP_FFT_STATIC_APP
+#define BSGP_FFT_STATIC_APP 0
+#endif
+BSGP_HD bool fft_static_len(int n) {
+  return n == 256 || n == 270 || (BSGP_FFT_STATIC_APP && (n == 400 || n == 480));
+}
 
 BSGP_HD cd tw_at(const cd* tw, int k, bool inv) {
   cd w = tw[k];
@@ -111,7 +120,8 @@ BSGP_HD void bfly5(cd* v, bool inv) {
 }
 
 // exp(-2*pi*i*m/R) (forward) or its conjugate, for the internal twiddles of
-// the composite butterflies (R = 6: m = 1, 2; R = 9: m = 1, 2, 4).
+// the composite butterflies (R = 6: m = 1, 2; R = 8: m = 1..3; R = 9: m = 1, 2,
+// 4; R = 10: m = 1..4).
 template <int R>
 BSGP_HD cd unit_root(int m, bool inv) {
   double c = 1.0, s = 0.0;
@@ -122,6 +132,11 @@ BSGP_HD cd unit_root(int m, bool inv) {
     const double h = 0.70710678118654752440;  // sqrt(2)/2
     c = m == 1 ? h : (m == 2 ? 0.0 : -h);
     s = m == 2 ? 1.0 : h;
+  } else if (R == 10) {  // m = 1..4
+    const double c36 = 0.80901699437494742410, s36 = 0.58778525229247312917;
+    const double c72 = 0.30901699437494742410, s72 = 0.95105651629515357212;
+    c = m == 1 ? c36 : (m == 2 ? c72 : (m == 3 ? -c72 : -c36));
+    s = (m == 1 || m == 4) ? s36 : s72;
   } else if (R == 9) {
     if (m == 1) {
       c = 0.76604444311897803520;
@@ -182,6 +197,7 @@ BSGP_HD void bfly_r(cd* v, bool inv) {
   if constexpr (R == 6) bfly_comp<3, 2>(v, inv);
   if constexpr (R == 8) bfly_comp<4, 2>(v, inv);
   if constexpr (R == 9) bfly_comp<3, 3>(v, inv);
+  if constexpr (R == 10) bfly_comp<5, 2>(v, inv);
 }
 
 // One Stockham stage with a compile-time radix. `lane` in [0, nlanes).
@@ -337,6 +353,17 @@ struct RadixList {
 // r8: radix-8 stages first (workgroup-wide transforms: 256 lanes, 2048 = 8*8*8*4).
 constexpr RadixList factor_radices(int n, bool comp = BSGP_FFT_COMPOSITE, bool r8 = false) {
   RadixList L{0, {}};
+  // one wave's 400- / 480-point transforms: three stages whose butterflies
+  // fill the 64 lanes in 4 rounds in all (nb = 50, 40, 80 and 60, 80, 48)
+  // instead of four radix-4/5/6 stages in 8 rounds
+  if (comp && !r8 && n == 400) {
+    L.n = 3; L.r[0] = 8; L.r[1] = 10; L.r[2] = 5;
+    return L;
+  }
+  if (comp && !r8 && n == 480) {
+    L.n = 3; L.r[0] = 8; L.r[1] = 6; L.r[2] = 10;
+    return L;
+  }
   int m = n;
   while (r8 && m % 8 == 0) { L.r[L.n++] = 8; m /= 8; }
   while (m % 4 == 0) { L.r[L.n++] = 4; m /= 4; }
@@ -434,11 +461,17 @@ BSGP_HD cd* fft_any(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlan
     if (p.n == 270) return fft_run_static<270, COMP>(a, b, t, inv, lane, nlanes, sync);
     return fft_run(a, b, p, inv, lane, nlanes, sync, t);
   }
+#if BSGP_FFT_STATIC_APP
+  if (p.n == 400) return fft_run_static<400, COMP>(a, b, p.tw, inv, lane, nlanes, sync);
+  if (p.n == 480) return fft_run_static<480, COMP>(a, b, p.tw, inv, lane, nlanes, sync);
+#endif
   return fft_run(a, b, p, inv, lane, nlanes, sync);
 #else
   switch (p.n) {
     case 256: return fft_run_static<256, COMP>(a, b, p.tw, inv, lane, nlanes, sync);
     case 270: return fft_run_static<270, COMP>(a, b, p.tw, inv, lane, nlanes, sync);
+    case 400: return fft_run_static<400, COMP>(a, b, p.tw, inv, lane, nlanes, sync);
+    case 480: return fft_run_static<480, COMP>(a, b, p.tw, inv, lane, nlanes, sync);
     default: return fft_run(a, b, p, inv, lane, nlanes, sync);
   }
 #endif

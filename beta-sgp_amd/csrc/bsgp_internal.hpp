@@ -148,7 +148,8 @@ void persist_kernels_all(std::vector<const void*>& f);
 // not four) take them instead of the cooperative build when this is <= 3
 // (runtime override: BSGP_PERWAVE_MIN_WG)
 #ifndef BSGP_PERWAVE_MIN_WG
-#define BSGP_PERWAVE_MIN_WG 4
+#define BSGP_PERWAVE_MIN_WG 2  // per-wave over cooperative (A/B): 375^2 tiles at 3 WG/CU, 1024 per
+                               // launch, 68.6 k -> 87.5 k image-it/s; 450^2 at 2 WG/CU 48.3 -> 59.7 k
 #endif
 #ifndef BSGP_COOP_GROUPS
 #define BSGP_COOP_GROUPS 4
@@ -162,6 +163,12 @@ void persist_kernels_all(std::vector<const void*>& f);
 constexpr int kCoopBlock = BSGP_COOP512 ? 512 : kBlock;
 // threads per workgroup of a plan's phase kernels
 __host__ __device__ inline int plan_block(const Geo& g) { return g.coop ? kCoopBlock : kBlock; }
+// plans whose persistent solve runs the application-size build (bsgp_persist_app.hip):
+// per-wave, float64 storage, a 400- or 480-point row or column transform
+inline bool app_static_plan(const Geo& g, int storage) {
+  const bool app_n = g.fp.n == 400 || g.fp.n == 480 || g.fq.n == 400 || g.fq.n == 480;
+  return !g.coop && storage == BSGP_STORAGE_F64 && app_n;
+}
 
 }  // namespace bsgp
 
@@ -181,5 +188,12 @@ hipError_t bsgp_c512_launch_persist(const void* a, int K, size_t lds, hipStream_
                                     unsigned* queue, unsigned* done, int grid);
 hipError_t bsgp_c512_persist_resident(const void* a, int K, size_t lds, int* per_cu);
 hipError_t bsgp_c512_persist_set_lds_limit(size_t bytes);
+// the application-size persistent build (bsgp_persist_app.hip): per-wave plans
+// of float64 storage whose row or column transform has 400 or 480 points
+size_t bsgp_app_args_size(void);
+hipError_t bsgp_app_launch_persist(const void* a, int K, size_t lds, hipStream_t s,
+                                   unsigned* queue, unsigned* done, int grid);
+hipError_t bsgp_app_persist_resident(const void* a, int K, size_t lds, int* per_cu);
+hipError_t bsgp_app_persist_set_lds_limit(size_t bytes);
 hipError_t bsgp_c512_phase_prof(unsigned long long* out, int n, int reset);
 }

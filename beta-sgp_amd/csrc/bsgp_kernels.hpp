@@ -51,6 +51,9 @@ namespace bsgp {
 #ifndef BSGP_LS_ATTR
 #define BSGP_LS_ATTR __attribute__((amdgpu_waves_per_eu(COOP ? 1 : ((K <= 2 && !ADAPT) ? 3 : 2))))
 #endif
+#ifndef BSGP_SERIES_BOUND
+#define BSGP_SERIES_BOUND 1  // closed-form trials past lam*max|u| <= 0.01 under the tail bound
+#endif
 #ifndef BSGP_ACC_SERIES
 #define BSGP_ACC_SERIES 0  // den^(b-1) by the series at series-step accepts: same speed on C3 (A/B), off
 #endif
@@ -1076,6 +1079,19 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
   // over the image (truncation < 1e-17 relative at MS = 6: (0.01)^7 * binom).
   constexpr int MS = 6;
   constexpr double kSeriesRho = 0.01;
+  // Beyond lam * max|u| <= kSeriesRho the series is still exact to rounding
+  // when the terms past m = MS are small: with |binom(b, m+1) / binom(b, m)|
+  // <= 1 for m >= MS + 1 (0 <= b <= MS + 2; also for b - 1) and
+  // sum w |u|^(MS+1) <= max|u| * P_MS
+  // (P_MS = sum w u^MS >= 0), the tail of each series is at most
+  //   |binom(b, MS+1)| lam^(MS+1) max|u| P_MS / (1 - lam max|u|),
+  // and trials whose tails stay below 2^-60 of the leading moment are taken
+  // in closed form too.  The bound is driven by the few pixels with large u:
+  // on C3's stagnating iterations (max|u| ~ 0.04 from ~80 pixels, the rest
+  // <= 0.004) it covers every trial after the first, where lam * max|u| <=
+  // kSeriesRho left lam = 0.4 to a direct pass (0.46 passes per iteration).
+  constexpr double kSeriesTail = 8.673617379884035e-19;  // 2^-60
+  const bool tail_bound = BSGP_SERIES_BOUND && obj.beta >= 0.0 && obj.beta <= MS + 2;
   const bool series = (MODE == 3 || MODE == 4) && !adapt && P.ls_series != 0;
   // the moments and binomial coefficients are the same in every thread: they
   // live in LDS after the first pass (ser[0..3][MS+1] = P, Q, binom(b, m),
@@ -1161,7 +1177,8 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
       }
     }
   }
-  // binomial coefficients of the series
+  // binomial coefficients of the series (and, for the tail bound, the
+  // scaled leading terms |binom(., MS+1)| P_MS / P_0 of both series)
   if (series && threadIdx.x == 0) {
     double c0 = 1.0, c1 = 1.0;
     ser[2 * (MS + 1)] = 1.0;
@@ -1172,11 +1189,28 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
       ser[2 * (MS + 1) + m] = c0;
       ser[3 * (MS + 1) + m] = c1;
     }
+    const double c7p = fabs(c0 * (obj.beta - MS) / (MS + 1));
+    const double c7q = fabs(c1 * (obj.beta - 1 - MS) / (MS + 1));
+    const double tp = c7p * ser[MS] / ser[0], tq = c7q * ser[2 * MS + 1] / ser[MS + 1];
+    // (a NaN or non-positive leading moment: no closed form past kSeriesRho)
+    ser[4 * (MS + 1)] = (ser[0] > 0 && ser[MS + 1] > 0 && tp == tp && tq == tq)
+                            ? (tp > tq ? tp : tq)
+                            : INFINITY;
   }
   __syncthreads();
+  const double tail_c = (series && tail_bound) ? ser[4 * (MS + 1)] : INFINITY;
+  auto series_ok = [&](double l) __attribute__((always_inline)) {
+    const double lu = l * rho;
+    if (lu <= kSeriesRho) return true;
+    if (!(lu <= 0.5)) return false;
+    double l7 = l;
+#pragma unroll
+    for (int m = 1; m <= MS; ++m) l7 *= l;
+    return l7 * rho * tail_c / (1.0 - lu) <= kSeriesTail;
+  };
   PH_T(tk1);
   while (!accepted) {
-    if (series && lam * rho <= kSeriesRho) {
+    if (series && series_ok(lam)) {
       // closed-form trial: no pass over the image
       double s0 = 0.0, s1 = 0.0, lm = 1.0;
       for (int m = 0; m <= MS; ++m) {

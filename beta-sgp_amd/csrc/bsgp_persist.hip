@@ -28,6 +28,8 @@ static int persist_mode(const SolveArgs& a, bool* adapt) {
 hipError_t launch_persist(const SolveArgs& a, int K, size_t lds, hipStream_t s, unsigned* queue,
                           unsigned* done, int grid) {
   if (a.g.coop) return bsgp_c512_launch_persist(&a, K, lds, s, queue, done, grid);
+  if (app_static_plan(a.g, a.storage))
+    return bsgp_app_launch_persist(&a, K, lds, s, queue, done, grid);
   if (a.storage == BSGP_STORAGE_F32) return launch_persist_f32(a, K, lds, s, queue, done, grid);
   return launch_persist_t<double>(a, K, lds, s, queue, done, grid);
 }
@@ -35,6 +37,7 @@ hipError_t launch_persist(const SolveArgs& a, int K, size_t lds, hipStream_t s, 
 // Workgroups of the persistent kernel a solve would launch that one CU holds.
 hipError_t persist_resident_per_cu(const SolveArgs& a, int K, size_t lds, int* per_cu) {
   if (a.g.coop) return bsgp_c512_persist_resident(&a, K, lds, per_cu);
+  if (app_static_plan(a.g, a.storage)) return bsgp_app_persist_resident(&a, K, lds, per_cu);
   bool adapt = false;
   const int mode = persist_mode(a, &adapt);
   const void* f = a.storage == BSGP_STORAGE_F32 ? persist_kernel_f32(K, mode, adapt)

@@ -425,6 +425,7 @@ hipError_t set_solver_lds_limit(size_t bytes) {
   }
   hipError_t e = BSGP_COOP512 ? bsgp_c512_set_lds_limit(bytes) : hipSuccess;
   if (e == hipSuccess && BSGP_COOP512) e = bsgp_c512_persist_set_lds_limit(bytes);
+  if (e == hipSuccess) e = bsgp_app_persist_set_lds_limit(bytes);
   if (e == hipSuccess) applied[dev] = bytes;
   return e;
 }

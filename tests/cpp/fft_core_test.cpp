@@ -83,9 +83,10 @@ int main() {
     for (int j = 0; j < Q; ++j) e2 = fmax(e2, fabs(zr[j].x / Q - ra[j]) + fabs(zr[j].y / Q - rb[j]));
     if (!(e1 < 1e-12 && e2 < 1e-14)) { printf("FAIL split Q=%d e1=%g e2=%g\n", Q, e1, e2); bad++; }
   }
-  // compile-time paths (composite radix-6/9 stages for 270) vs the naive DFT
+  // compile-time paths (composite radix-6/9 stages for 270, 8/10/5 for 400,
+  // 8/6/10 for 480) vs the naive DFT
   // and vs the runtime plan
-  for (int n : {256, 270}) {
+  for (int n : {256, 270, 400, 480}) {
     for (int inv = 0; inv < 2; ++inv) {
       FftPlan p;
       p.n = n;

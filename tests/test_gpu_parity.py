@@ -195,21 +195,26 @@ def test_satellite_332_known_answer(sgpmod, name):
     """simulation_test_sgp.py:37-56 / 112-169: the satellite for 332
     iterations, rel. error vs ground truth 0.2904372552 (KL) and
     0.2910767378 (beta = 1.0001).  At 332 iterations the runs are chaotic
-    (SURVEY §4): the reference itself with scipy.fft in place of numpy's FFT
-    lands rel_err 2.1e-4 / 3.2e-4 away (recorded in the fixture).  The
-    device's FFT rounds differently again, so its rel_err must lie within 3x
-    that spread of the reference's, and its discrepancy follow the
-    reference's through iteration 50 (before the chaos) at rtol 1e-7."""
+    (SURVEY §4): the reference itself, fed the observed image changed by one
+    ulp per pixel (8 random-sign seeds, make_golden.py satellite), lands
+    rel_err in [0.2900, 0.2956] (KL) / [0.2898, 0.2971] (beta) and moves x by
+    up to 7.7e-2 / 6.8e-2.  The device's FFT and sums round differently, so
+    its rel_err and x must lie within 1.5x that ensemble's largest deviation
+    from the reference's run; its discrepancy follows the reference's through
+    iteration 50 (before the chaos: 1.8e-11 in that ensemble) at 1e-7."""
     from conftest import satellite_case
     gn, psf, bkg, obj, kw, fn, fx = satellite_case(name)
     x, it, discr, _, _ = getattr(sgpmod, fn)(gn, psf, bkg, **kw)
     assert it == 332 and len(discr) == 333
-    relerr = float(np.sqrt(np.sum((x - obj) ** 2) / np.sum(obj * obj)))
-    spread = abs(float(fx["relerr_scipyfft"]) - float(fx["relerr"]))
-    print(name, "rel_err", relerr, "reference", float(fx["relerr"]), "spread", spread,
-          "x rel", rel(x, fx["x"]))
-    assert abs(relerr - float(fx["relerr"])) <= 3 * spread, (relerr, spread)
     np.testing.assert_allclose(discr[:51], fx["discr"][:51], rtol=1e-7)
+    relerr = float(np.sqrt(np.sum((x - obj) ** 2) / np.sum(obj * obj)))
+    ref = float(fx["relerr"])
+    spread = float(np.max(np.abs(fx["relerr_ulp_ensemble"] - ref)))
+    xspread = float(np.max(fx["x_rel_ulp_ensemble"]))
+    print(name, "rel_err", relerr, "reference", ref, "ensemble spread", spread, "x rel",
+          rel(x, fx["x"]), "ensemble x rel", xspread)
+    assert abs(relerr - ref) <= 1.5 * spread, (relerr, ref, spread)
+    assert rel(x, fx["x"]) <= 1.5 * xspread, (rel(x, fx["x"]), xspread)
 
 
 def test_stamp31_odd_size_adaptive_beta(sgpmod):

@@ -235,4 +235,5 @@ def test_oracle_satellite_332_iterations(name):
     rel = float(np.sqrt(np.sum(e * e) / np.sum(obj * obj)))
     spread = abs(float(fx["relerr_scipyfft"]) - float(fx["relerr"]))
     assert abs(rel - float(fx["relerr"])) <= spread, (rel, float(fx["relerr"]), spread)
+    assert np.all(np.abs(fx["relerr_ulp_ensemble"] - float(fx["relerr"])) < 1e-2)
     np.testing.assert_allclose(discr[:51], fx["discr"][:51], rtol=1e-7)

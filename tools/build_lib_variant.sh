@@ -9,7 +9,7 @@ NAME=$1; FLAGS=$2; SRC=${3:-$R}
 B=/tmp/bsgp_build_$NAME; mkdir -p $B
 CF="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -mcode-object-version=5"
 OBJS=()
-for f in bsgp_solver bsgp_solver_f32 bsgp_solver_c512 bsgp_persist bsgp_persist_f32 bsgp_api bsgp_tiles bsgp_psf; do
+for f in bsgp_solver bsgp_solver_f32 bsgp_solver_c512 bsgp_persist bsgp_persist_f32 bsgp_persist_c512 bsgp_persist_c512_f32 bsgp_persist_app bsgp_api bsgp_tiles bsgp_psf; do
   /opt/rocm/bin/hipcc $CF $FLAGS -I $SRC/include -c $SRC/beta-sgp_amd/csrc/$f.hip -o $B/$f.o &
   OBJS+=($B/$f.o)
 done

@@ -8,7 +8,7 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 B=$R/build
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -mcode-object-version=5"
-OTHERS="$B/bsgp_solver.o $B/bsgp_solver_f32.o $B/bsgp_solver_c512.o $B/bsgp_persist_f32.o $B/bsgp_api.o $B/bsgp_tiles.o $B/bsgp_psf.o"
+OTHERS="$B/bsgp_solver.o $B/bsgp_solver_f32.o $B/bsgp_solver_c512.o $B/bsgp_persist_f32.o $B/bsgp_persist_c512.o $B/bsgp_persist_c512_f32.o $B/bsgp_persist_app.o $B/bsgp_api.o $B/bsgp_tiles.o $B/bsgp_psf.o"
 while [ $# -ge 2 ]; do
   ( /opt/rocm/bin/hipcc $FLAGS $2 -I $R/include -c $R/beta-sgp_amd/csrc/bsgp_persist.hip -o $B/persist_$1.o &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/beta-sgp_amd/libbsgp_$1.so $B/persist_$1.o $OTHERS ) &

@@ -12,6 +12,7 @@ compare with bench.py's per-kernel algorithmic bytes (run the PMC passes with
 --streams 1 so a launch is the whole batch, as in bench.py's profiled solve).
 """
 import csv
+import re
 import json
 import sys
 from collections import defaultdict
@@ -26,7 +27,8 @@ def load(f, ctr):
         if r["Counter_Name"] != ctr:
             continue
         name = r["Kernel_Name"]
-        key = next((k for k in SOLVER if f"bsgp::{k}" in name), None)
+        # any build namespace: bsgp, bsgp_c512 (cooperative), bsgp_app (400/480 grids)
+        key = next((k for k in SOLVER if re.search(r"bsgp\w*::" + k + r"<", name)), None)
         if key is None:
             continue
         tot[key] += float(r["Counter_Value"]) * 1024.0
