@@ -104,6 +104,16 @@ CONFIGS = {
                           "circular A"),
 }
 STAMP_PUBLISHED = 1167.5  # it/s, beta-SGP star stamps (results/EXEC_TIME_BETA.npy, NUM_ITERS_BETA.npy)
+# the reference's own published single-frame rates for the subdivision application (context
+# only: one image on unstated hardware, so vs_baseline stays null for these lines)
+PUBLISHED_CONTEXT = {
+    "sub375": "reference: one 375x375 subdivision, beta-SGP 43 iterations in 6.70 s = 6.42 it/s, "
+              "KL 51 in 6.54 s = 7.80 it/s (results/SUBDIV_EXEC_TIME*.npy, SUBDIV_NUM_ITERS*.npy; "
+              "hardware unstated)",
+    "sub450": "reference: the 450x450 CROWDED frame, beta-SGP 51 iterations in 10.25 s = 4.98 it/s, "
+              "KL 2 in 0.571 s = 3.50 it/s (results/CROWDED_SUBDIV_EXEC_TIME*.npy, "
+              "CROWDED_SUBDIV_NUM_ITERS*.npy; hardware unstated)",
+}
 
 
 def stamp_inputs(B, seed=0):
@@ -538,6 +548,8 @@ def main():
         "roofline": None,
         "cpu_baseline": None,
     }
+    if args.config in PUBLISHED_CONTEXT:
+        result["context"] = PUBLISHED_CONTEXT[args.config]
     if args.stub:
         result["data"] = "stub: harness test without a GPU"
         print(json.dumps(result), flush=True)

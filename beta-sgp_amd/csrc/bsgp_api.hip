@@ -368,14 +368,23 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   // per-wave transforms at three workgroups per CU (12 waves/CU) before the
   // cooperative build's one 512-thread workgroup per CU (8 waves): 375^2 tiles
   // on their 400-point grid fit (52.9 KB of 54.3 KB)
+  // With BSGP_PERWAVE_TW the twiddle tables must fit beside the buffers too:
+  // a wave's transform that reads its twiddles from global memory waits on
+  // them in every stage (375^2 tiles at 3 WG/CU: the 400-point row and column
+  // transforms took 3.5x the cycles per point of C3's 270-point ones, phase
+  // profile), so two workgroups per CU with LDS twiddles can beat three without.
+  const size_t twb_all = (size_t)(g.P == g.Q ? g.P : g.P + g.Q) * sizeof(cd);
   {
     const char* e = getenv("BSGP_PERWAVE_MIN_WG");
     const int min_wg = e ? atoi(e) : BSGP_PERWAVE_MIN_WG;
+    const char* et = getenv("BSGP_PERWAVE_TW");
+    const size_t tw_need = (et ? atoi(et) : BSGP_PERWAVE_TW) ? twb_all : 0;
     for (int wg = 3; wg >= 2 && wg >= min_wg; --wg) {
       const size_t bw = 160 * 1024 / wg - 256;
-      if (need(kWaves) > budget && need(kWaves) <= bw) {
+      if (need(kWaves) > budget && need(kWaves) + tw_need <= bw) {
         budget = bw;
         p->wg_per_cu = wg;
+        break;
       }
     }
   }

@@ -459,6 +459,10 @@ BSGP_HD cd* fft_any(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlan
     const cd* t = reinterpret_cast<const cd*>(bsgp_dyn_lds + p.lds_tw);
     if (p.n == 256) return fft_run_static<256, COMP>(a, b, t, inv, lane, nlanes, sync);
     if (p.n == 270) return fft_run_static<270, COMP>(a, b, t, inv, lane, nlanes, sync);
+#if BSGP_FFT_STATIC_APP
+    if (p.n == 400) return fft_run_static<400, COMP>(a, b, t, inv, lane, nlanes, sync);
+    if (p.n == 480) return fft_run_static<480, COMP>(a, b, t, inv, lane, nlanes, sync);
+#endif
     return fft_run(a, b, p, inv, lane, nlanes, sync, t);
   }
 #if BSGP_FFT_STATIC_APP

@@ -151,6 +151,9 @@ void persist_kernels_all(std::vector<const void*>& f);
 #define BSGP_PERWAVE_MIN_WG 2  // per-wave over cooperative (A/B): 375^2 tiles at 3 WG/CU, 1024 per
                                // launch, 68.6 k -> 87.5 k image-it/s; 450^2 at 2 WG/CU 48.3 -> 59.7 k
 #endif
+#ifndef BSGP_PERWAVE_TW
+#define BSGP_PERWAVE_TW 1
+#endif
 #ifndef BSGP_COOP_GROUPS
 #define BSGP_COOP_GROUPS 4
 #endif
@@ -195,5 +198,6 @@ hipError_t bsgp_app_launch_persist(const void* a, int K, size_t lds, hipStream_t
                                    unsigned* queue, unsigned* done, int grid);
 hipError_t bsgp_app_persist_resident(const void* a, int K, size_t lds, int* per_cu);
 hipError_t bsgp_app_persist_set_lds_limit(size_t bytes);
+hipError_t bsgp_app_phase_prof(unsigned long long* out, int n, int reset);
 hipError_t bsgp_c512_phase_prof(unsigned long long* out, int n, int reset);
 }

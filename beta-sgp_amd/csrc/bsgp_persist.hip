@@ -60,6 +60,11 @@ hipError_t persist_phase_prof(unsigned long long* out, int n, int reset) {
     e = persist_phase_prof_f32(c, n, reset);
     for (int i = 0; i < n; ++i) out[i] += c[i];
   }
+  if (e == hipSuccess) {
+    unsigned long long c[kPhaseSlots] = {};
+    e = bsgp_app_phase_prof(c, n, reset);
+    for (int i = 0; i < n; ++i) out[i] += c[i];
+  }
   return e;
 #else
   for (int i = 0; i < n; ++i) out[i] = 0;

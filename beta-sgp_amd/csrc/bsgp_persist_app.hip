@@ -57,4 +57,21 @@ hipError_t bsgp_app_persist_set_lds_limit(size_t bytes) {
   return hipSuccess;
 }
 
+// phase-profile counters of this build (-DBSGP_PHASE_PROF; persist_phase_prof adds them)
+hipError_t bsgp_app_phase_prof(unsigned long long* out, int n, int reset) {
+#ifdef BSGP_PHASE_PROF
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(bsgp_app::g_phase),
+                                     n * sizeof(unsigned long long));
+  if (e == hipSuccess && reset) {
+    unsigned long long z[bsgp_app::kPhaseSlots] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(bsgp_app::g_phase), z, sizeof z);
+  }
+  return e;
+#else
+  for (int i = 0; i < n; ++i) out[i] = 0;
+  (void)reset;
+  return hipSuccess;
+#endif
+}
+
 }  // extern "C"

@@ -434,6 +434,32 @@ def make_long():
               f"discrN={discr[-1]:.12f}")
 
 
+def make_long_ensemble():
+    """The reference's own spread on the timed workload to MAXIT 100: each
+    c3long fixture's run repeated with the observed image changed by one ulp
+    per pixel (random sign, seeds 0..5).  Seed 2's trajectory is unstable near
+    iteration 55 (a faithful restatement parts from it there); the spread
+    recorded here is what a rounding-level change does to the reference
+    itself, i.e. the tolerance a device run can be held to on that fixture."""
+    sgp, fcp = import_reference(need_astropy=True)
+    for name in ["c3long_s0", "c3long_s1", "c3long_s2"]:
+        z = np.load(os.path.join(OUT, f"ref_{name}.npz"))
+        import ast
+        kw = ast.literal_eval(str(z["kwargs"]))
+        gn = z["gn"].astype(np.float64)
+        xr, dr = [], []
+        for seed in range(6):
+            sg = np.random.default_rng(seed).choice([-1.0, 1.0], gn.shape)
+            x, it, discr, _, _ = run_quiet(sgp.sgp_betaDiv, gn * (1.0 + sg * 2.0 ** -52), z["psf"],
+                                           np.float64(100.0), **kw)
+            assert it == int(z["iters"])
+            xr.append(float(np.linalg.norm(x - z["x"]) / np.linalg.norm(z["x"])))
+            dr.append(float(np.max(np.abs(discr / z["discr"] - 1))))
+        np.savez_compressed(os.path.join(OUT, f"ref_{name}_ens.npz"), x_rel=np.array(xr),
+                            discr_rel=np.array(dr))
+        print(f"{name}: one-ulp ensemble x rel max {max(xr):.2e}, discr rel max {max(dr):.2e}")
+
+
 def star_positions(img, n, half=15, sep=31):
     """Bright local maxima of img whose (2*half+1)^2 cutout lies inside the
     frame, at least sep pixels apart, brightest first: (x, y) = (col, row)."""
@@ -769,6 +795,8 @@ if __name__ == "__main__":
                 make_errsave()
             elif which == "long":
                 make_long()
+            elif which == "long_ens":
+                make_long_ensemble()
             elif which == "c4":
                 make_c4()
             elif which == "stamps":
