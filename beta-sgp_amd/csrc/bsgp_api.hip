@@ -183,11 +183,6 @@ struct bsgp_plan_s {
   // persistent solver: dequeue counter + per-image published iterations
   unsigned* pq = nullptr;
   size_t pq_n = 0;
-  // 400-point per-wave plans at three workgroups per CU: the compact root table
-  // (fft400_compact) in LDS for the application-size persistent build only
-  cd* twc = nullptr;
-  int twc_off = -1;          // its LDS byte offset in that build's launches
-  size_t lds_bytes_app = 0;  // their dynamic LDS (lds_bytes + the table)
 };
 
 // Capacity of one thread's projection list: the pixels it streams in one pass
@@ -384,21 +379,11 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
     const int min_wg = e ? atoi(e) : BSGP_PERWAVE_MIN_WG;
     const char* et = getenv("BSGP_PERWAVE_TW");
     const size_t tw_need = (et ? atoi(et) : BSGP_PERWAVE_TW) ? twb_all : 0;
-    // 400-point grids (375^2 tiles): the compact root table fits three per CU
-    const char* ec = getenv("BSGP_TW400C");
-    const bool c400 = g.P == 400 && g.Q == 400 && (ec ? atoi(ec) : BSGP_TW400C) && tw_need > 0;
-    const size_t twc_b = (size_t)kTw400Compact * sizeof(cd);
     for (int wg = 3; wg >= 2 && wg >= min_wg; --wg) {
       const size_t bw = 160 * 1024 / wg - 256;
       if (need(kWaves) > budget && need(kWaves) + tw_need <= bw) {
         budget = bw;
         p->wg_per_cu = wg;
-        break;
-      }
-      if (c400 && need(kWaves) > budget && need(kWaves) + twc_b <= bw) {
-        budget = bw;
-        p->wg_per_cu = wg;
-        p->twc_off = 0;  // placed below
         break;
       }
     }
@@ -440,12 +425,7 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   // budget (one table when P == Q), else they read the global table (as the
   // cooperative workgroup-wide transforms always do)
   g.fp.lds_tw = g.fq.lds_tw = -1;
-  g.fp.tw_compact = g.fq.tw_compact = 0;
-  p->lds_bytes_app = 0;
-  if (p->twc_off == 0) {  // compact 400-point roots: only the application-size persistent build
-    p->twc_off = (int)p->lds_bytes;
-    p->lds_bytes_app = p->lds_bytes + (size_t)kTw400Compact * sizeof(cd);
-  } else if (!g.coop) {
+  if (!g.coop) {
     const size_t twb = (size_t)(g.P == g.Q ? g.P : g.P + g.Q) * sizeof(cd);
     if (p->lds_bytes + twb <= budget) {
       g.fp.lds_tw = (int)p->lds_bytes;
@@ -468,7 +448,7 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
     delete p;
     return fail(BSGP_ERR_HIP, "application-size persistent build does not match this library");
   }
-  if (set_solver_lds_limit(std::max(p->lds_bytes, p->lds_bytes_app)) != hipSuccess) {
+  if (set_solver_lds_limit(p->lds_bytes) != hipSuccess) {
     delete p;
     return fail(BSGP_ERR_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
   }
@@ -490,24 +470,6 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
     }
     g.fp.tw = p->tw;
     g.fq.tw = p->tw + g.P;
-    g.fp.tw_src = g.fp.tw;
-    g.fq.tw_src = g.fq.tw;
-    g.fp.tw_src_n = g.P;
-    g.fq.tw_src_n = g.Q;
-    if (p->twc_off >= 0) {
-      std::vector<cd> c(kTw400Compact);
-      const long double pi = 3.141592653589793238462643383279502884L;
-      for (int k = 0; k < 8; ++k)
-        c[k] = cmk((double)cosl(-2.0L * pi * k / 80.0L), (double)sinl(-2.0L * pi * k / 80.0L));
-      for (int k = 0; k < 80; ++k)
-        c[8 + k] = tw[k];  // w400^k (the P = 400 table)
-      if (hipMalloc(&p->twc, c.size() * sizeof(cd)) != hipSuccess ||
-          hipMemcpy(p->twc, c.data(), c.size() * sizeof(cd), hipMemcpyHostToDevice) !=
-              hipSuccess) {
-        bsgp_plan_destroy(p);
-        return fail(BSGP_ERR_HIP, "twiddle upload failed");
-      }
-    }
   }
   // circularly-placed kernels for A and AT on the P x Q grid
   const size_t PQ = (size_t)g.P * g.Q;
@@ -604,7 +566,6 @@ int bsgp_plan_destroy(bsgp_plan p) {
   if (!p) return BSGP_OK;
   DeviceGuard dev_guard_(p->device);
   if (p->tw) (void)hipFree(p->tw);
-  if (p->twc) (void)hipFree(p->twc);
   if (p->tf) (void)hipFree(p->tf);
   if (p->ws) (void)hipFree(p->ws);
   for (int i = 1; i < p->nsub; ++i) {
@@ -891,27 +852,14 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
       p->pq_n = need;
     }
     HIP_TRY(hipMemsetAsync(p->pq, 0, need * sizeof(unsigned), s));
-    // the application-size build of a 400-point plan reads the compact roots
-    // from LDS (fft400_compact); every other launch of the plan reads the
-    // full table from global memory
-    size_t lds_p = p->lds_bytes;
-    if (p->twc && app_static_plan(p->g, p->storage)) {
-      for (FftPlan* f : {&sa[0].g.fp, &sa[0].g.fq}) {
-        f->lds_tw = p->twc_off;
-        f->tw_src = p->twc;
-        f->tw_src_n = kTw400Compact;
-        f->tw_compact = 1;
-      }
-      lds_p = p->lds_bytes_app;
-    }
     int per_cu = 0;
-    HIP_TRY(persist_resident_per_cu(sa[0], K, lds_p, &per_cu));
+    HIP_TRY(persist_resident_per_cu(sa[0], K, p->lds_bytes, &per_cu));
     if (per_cu < 1) return fail(BSGP_ERR_HIP, "persistent solver does not fit a CU");
     // every workgroup resident at once (a dequeued task's predecessor is always
     // running or done); no more workgroups than images
     const int grid = (int)std::min<long>(B, (long)p->ncu * per_cu);
     if (prof) HIP_TRY(hipEventRecord(prof->ev[2], s));
-    HIP_TRY(launch_persist(sa[0], K, lds_p, s, p->pq, p->pq + 1, grid));
+    HIP_TRY(launch_persist(sa[0], K, p->lds_bytes, s, p->pq, p->pq + 1, grid));
     if (prof) {
       HIP_TRY(hipEventRecord(prof->ev[3], s));
       HIP_TRY(hipStreamSynchronize(s));

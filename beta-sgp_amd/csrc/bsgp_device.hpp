@@ -85,7 +85,7 @@ __device__ __forceinline__ void copy_tw(const FftPlan& f) {
   if (f.lds_tw < 0) return;
   extern __shared__ __attribute__((aligned(16))) char bsgp_dyn_lds[];
   cd* d = reinterpret_cast<cd*>(bsgp_dyn_lds + f.lds_tw);
-  for (int i = threadIdx.x; i < f.tw_src_n; i += kBlock) d[i] = f.tw_src[i];
+  for (int i = threadIdx.x; i < f.n; i += kBlock) d[i] = f.tw[i];
 }
 __device__ __forceinline__ void load_tw_lds(const Geo& G) {
   copy_tw(G.fp);

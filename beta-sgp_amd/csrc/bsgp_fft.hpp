@@ -53,19 +53,7 @@ struct FftPlan {
   int radix[kMaxStages];
   const cd* tw;  // n entries, exp(-2*pi*i*k/n)
   int lds_tw;    // device: byte offset of a copy of tw in dynamic LDS, or -1
-  // device: the LDS copy's source and length -- tw and n, or (tw_compact = 1,
-  // n = 400) the compact root table of fft400_compact
-  const cd* tw_src;
-  int tw_src_n;
-  int tw_compact;
 };
-
-// Compact roots of the 400-point transform (8 * 10 * 5): c[jm] = w80^jm
-// (jm < 8, stage 2) and c[8 + jm] = w400^jm (jm < 80, stage 3); a stage's
-// twiddle w^(r jm) is the r-th power of its root, by repeated complex
-// multiplication.  88 entries (1.4 KB) instead of 400 (6.4 KB): the LDS left
-// over by three workgroups of 375^2 tiles per CU holds them.
-constexpr int kTw400Compact = 88;
 
 // Lengths with a compile-time transform (the hot grid sizes: 256 for circular
 // 256^2 images, 270 for 256^2 images with a 25x25 PSF in linear mode, and
@@ -449,57 +437,6 @@ BSGP_HD cd* fft_run_static(cd* a, cd* b, const cd* tw, bool inv, int lane, int n
   return stages_static<N, 0, 1, COMP, R8>(a, b, tw, inv, lane, nlanes, sync);
 }
 
-// 400-point transform on the compact root table (stages 8, 10, 5).
-template <class Sync>
-BSGP_HD cd* fft400_compact(cd* a, cd* b, const cd* c, bool inv, int lane, int nlanes, Sync sync) {
-  constexpr int N = 400;
-  stage_static<8, N, 1>(a, b, c, inv, lane, nlanes);  // Ns = 1: no twiddles
-  sync();
-  {  // radix 10, Ns = 8: w400^(5 r jm) = (w80^jm)^r
-    constexpr int R = 10, Ns = 8, nb = N / R;
-    for (int j = lane; j < nb; j += nlanes) {
-      const int jm = j % Ns;
-      cd v[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) v[r] = b[j + r * nb];
-      const cd w = tw_at(c, jm, inv);
-      cd wr = w;
-#pragma unroll
-      for (int r = 1; r < R; ++r) {
-        v[r] = cmul(v[r], wr);
-        if (r + 1 < R) wr = cmul(wr, w);
-      }
-      bfly_r<R>(v, inv);
-      const int od = (j / Ns) * Ns * R + jm;
-#pragma unroll
-      for (int r = 0; r < R; ++r) a[od + r * Ns] = v[r];
-    }
-  }
-  sync();
-  {  // radix 5, Ns = 80: w400^(r jm)
-    constexpr int R = 5, Ns = 80, nb = N / R;
-    for (int j = lane; j < nb; j += nlanes) {
-      const int jm = j % Ns;
-      cd v[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) v[r] = a[j + r * nb];
-      const cd w = tw_at(c, 8 + jm, inv);
-      cd wr = w;
-#pragma unroll
-      for (int r = 1; r < R; ++r) {
-        v[r] = cmul(v[r], wr);
-        if (r + 1 < R) wr = cmul(wr, w);
-      }
-      bfly_r<R>(v, inv);
-      const int od = (j / Ns) * Ns * R + jm;
-#pragma unroll
-      for (int r = 0; r < R; ++r) b[od + r * Ns] = v[r];
-    }
-  }
-  sync();
-  return b;
-}
-
 // Workgroup-wide transform (all kBlock-style lanes, `sync` = workgroup
 // barrier): compile-time radix-8 plan for 2048 (config C4), runtime plan otherwise.
 template <class Sync>
@@ -523,9 +460,7 @@ BSGP_HD cd* fft_any(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlan
     if (p.n == 256) return fft_run_static<256, COMP>(a, b, t, inv, lane, nlanes, sync);
     if (p.n == 270) return fft_run_static<270, COMP>(a, b, t, inv, lane, nlanes, sync);
 #if BSGP_FFT_STATIC_APP
-    if (p.n == 400)
-      return p.tw_compact ? fft400_compact(a, b, t, inv, lane, nlanes, sync)
-                          : fft_run_static<400, COMP>(a, b, t, inv, lane, nlanes, sync);
+    if (p.n == 400) return fft_run_static<400, COMP>(a, b, t, inv, lane, nlanes, sync);
     if (p.n == 480) return fft_run_static<480, COMP>(a, b, t, inv, lane, nlanes, sync);
 #endif
     return fft_run(a, b, p, inv, lane, nlanes, sync, t);

@@ -154,11 +154,6 @@ void persist_kernels_all(std::vector<const void*>& f);
 #ifndef BSGP_PERWAVE_TW
 #define BSGP_PERWAVE_TW 1
 #endif
-// 400-point per-wave plans: three workgroups per CU with the compact root table
-// (bsgp_fft.hpp fft400_compact) in the application-size persistent build
-#ifndef BSGP_TW400C
-#define BSGP_TW400C 1
-#endif
 #ifndef BSGP_COOP_GROUPS
 #define BSGP_COOP_GROUPS 4
 #endif

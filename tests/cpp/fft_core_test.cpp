@@ -141,27 +141,6 @@ int main() {
       }
     }
   }
-  // the compact-root 400-point transform (fft400_compact: roots w80^jm and
-  // w400^jm, powers by repeated multiplication) vs the full-table static plan
-  for (int inv = 0; inv < 2; ++inv) {
-    const int n = 400;
-    std::vector<cd> tw = twiddles(n), c(kTw400Compact);
-    for (int k = 0; k < 8; ++k) {
-      long double a = -2.0L * 3.141592653589793238462643383279502884L * k / 80.0L;
-      c[k] = cmk((double)cosl(a), (double)sinl(a));
-    }
-    for (int k = 0; k < 80; ++k) c[8 + k] = tw[k];
-    std::vector<cd> a(n), b(n), e(n), f(n);
-    for (int i = 0; i < n; ++i) a[i] = e[i] = cmk(rand() / (double)RAND_MAX, rand() / (double)RAND_MAX);
-    cd* r1 = fft_run_static<400>(e.data(), f.data(), tw.data(), inv, 0, 1, [] {});
-    cd* r2 = fft400_compact(a.data(), b.data(), c.data(), inv, 0, 1, [] {});
-    double md = 0, mr = 0;
-    for (int k = 0; k < n; ++k) {
-      md = fmax(md, fabs(r1[k].x - r2[k].x) + fabs(r1[k].y - r2[k].y));
-      mr = fmax(mr, fabs(r1[k].x) + fabs(r1[k].y));
-    }
-    if (!(md / mr < 1e-14)) { printf("FAIL compact400 inv=%d rel %g\n", inv, md / mr); bad++; }
-  }
   printf(bad ? "FFT core: %d failures\n" : "FFT core: all ok\n", bad);
   return bad ? 1 : 0;
 }
