@@ -317,15 +317,40 @@ def storage_code(storage):
     return STORAGE[storage]
 
 
+# Plans are found by PSF content.  Keying the cache by the PSF's bytes cost
+# every call a copy and a hash of the whole PSF (C4's circular A takes a
+# 2048^2 PSF: ~20 ms of host time per call, GPU idle when the call starts
+# from an idle stream); the key holds a fingerprint of a strided sample
+# instead, and a plan matches only when its own copy of the PSF is
+# byte-identical to the caller's (memcmp: one pass over the PSF).
+_libc = ctypes.CDLL(None)
+_libc.memcmp.restype = ctypes.c_int
+_libc.memcmp.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+
+
+def _same_psf(plan, psf):
+    ref = plan._psf_host
+    return ref.shape == psf.shape and (
+        psf.nbytes == 0 or _libc.memcmp(ref.ctypes.data, psf.ctypes.data, psf.nbytes) == 0)
+
+
 def _plan_key(H, W, psf, conv_mode, storage):
     psf = np.ascontiguousarray(psf, dtype="<f8")
-    return psf, (H, W, psf.shape, psf.tobytes(), conv_mode, storage_code(storage),
+    flat = psf.reshape(-1)
+    sample = flat[::max(1, flat.size // 4096)].tobytes()
+    return psf, (H, W, psf.shape, hash(sample), conv_mode, storage_code(storage),
                  torch.cuda.current_device())
+
+
+def _new_plan(H, W, psf, key):
+    p = Plan(H, W, psf, key[4], key[6], storage=key[5])
+    p._psf_host = psf.copy()  # (the caller may rewrite its array later)
+    return p
 
 
 def get_plan(H, W, psf, conv_mode, storage="f64"):
     """A plan for the calling thread's own use (operators, plan queries):
-    cached per (shape, psf bytes, mode, storage, device, host thread), since a
+    cached per (shape, psf content, mode, storage, device, host thread), since a
     plan's operator workspace serves one call at a time (include/bsgp.h: a
     plan is not thread-safe).  Entries of threads that have ended are dropped.
     Solves take their plan from the shared pool (lease_plan) instead."""
@@ -334,13 +359,13 @@ def get_plan(H, W, psf, conv_mode, storage="f64"):
     key = key + (threading.get_ident(),)
     with _plan_cache_lock:
         p = _plan_cache.get(key)
-        if p is None:
+        if p is None or not _same_psf(p, psf):
             live = {t.ident for t in threading.enumerate()}
             for k in [k for k in _plan_cache if k[-1] not in live]:
                 del _plan_cache[k]
             if len(_plan_cache) > 16:
                 _plan_cache.clear()
-            p = Plan(H, W, psf, conv_mode, key[6], storage=key[5])
+            p = _new_plan(H, W, psf, key)
             _plan_cache[key] = p
     return p
 
@@ -369,9 +394,9 @@ class lease_plan:
         psf, key = _plan_key(H, W, psf, conv_mode, storage)
         with _plan_cache_lock:
             plans = _pool.setdefault(key, [])
-            p = next((q for q in plans if not q._leased), None)
+            p = next((q for q in plans if not q._leased and _same_psf(q, psf)), None)
             if p is None:
-                p = Plan(H, W, psf, conv_mode, key[6], storage=key[5])
+                p = _new_plan(H, W, psf, key)
                 p._done = None
                 if len(plans) < _POOL_MAX:
                     plans.append(p)

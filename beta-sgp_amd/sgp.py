@@ -78,7 +78,11 @@ PERSIST_DEFAULT = 1  # one-workgroup batches: all iterations in one persistent l
 
 # ------------------------------------------------------------------ helpers
 def _check_psf(psf):
-    checkPSF = np.abs(np.sum(psf.flatten()) - 1.)
+    # (np.sum of a C-contiguous array is np.sum of its flatten(): the same
+    # pairwise order over the same buffer, without the copy)
+    total = np.sum(psf) if isinstance(psf, np.ndarray) and psf.flags.c_contiguous \
+        else np.sum(psf.flatten())
+    checkPSF = np.abs(total - 1.)
     tolCheckPSF = 1e4 * np.finfo(float).eps
     if checkPSF > tolCheckPSF:
         errmsg = f"\n\tsum(psf) - 1. = {checkPSF}, tolerance = {tolCheckPSF}"

@@ -120,6 +120,37 @@ def test_plan_pool_reuses_plans_across_threads(sgpmod):
         np.testing.assert_array_equal(a["x"], b["x"])
 
 
+def test_plan_cache_matches_psf_content(sgpmod):
+    """Plans are keyed by a fingerprint of a strided sample of the PSF and
+    matched by its full bytes: two PSFs that differ only off the sample share
+    a key but never a plan, in the per-thread cache and in the solve pool, and
+    a solve with the second PSF equals a solve on a fresh plan of it."""
+    import _bsgp
+    rng = np.random.default_rng(3)
+    psf = rng.random((128, 128))
+    psf /= psf.sum()
+    psf2 = psf.copy()
+    d = 0.5 * psf[0, 2]  # mass moved between elements 1 and 2, off the sample (every 4th)
+    psf2[0, 1] += d
+    psf2[0, 2] -= d
+    mode = _bsgp.BSGP_CONV_CIRCULAR
+    k1 = _bsgp._plan_key(128, 128, psf, mode, "f64")[1]
+    k2 = _bsgp._plan_key(128, 128, psf2, mode, "f64")[1]
+    assert k1 == k2
+    p1 = _bsgp.get_plan(128, 128, psf, mode)
+    p2 = _bsgp.get_plan(128, 128, psf2, mode)
+    assert p1 is not p2 and np.array_equal(p2._psf_host, psf2)
+    assert _bsgp.get_plan(128, 128, psf2, mode) is p2
+    gn = (rng.poisson(200.0, (1, 128, 128)) + 1.0).astype(np.float64)
+    kw = dict(init_recon=2, proj_type=1, stop_criterion=1, MAXIT=3, betaParams=1.05)
+    a = sgpmod.sgp_betaDiv_batch(gn, psf, 10.0, **kw)
+    b = sgpmod.sgp_betaDiv_batch(gn, psf2, 10.0, **kw)
+    _bsgp._pool.clear()
+    c = sgpmod.sgp_betaDiv_batch(gn, psf2, 10.0, **kw)
+    np.testing.assert_array_equal(b["x"], c["x"])
+    assert not np.array_equal(a["x"], b["x"])
+
+
 def test_device_scope_restores_current_device(sgpmod):
     """Every plan entry point restores the caller's current device: after a
     plan is created and destroyed from another thread, this thread's current
