@@ -382,11 +382,15 @@ _POOL_MAX = 8  # plans kept per key
 
 
 class lease_plan:
-    """Context manager: ``with lease_plan(H, W, psf, mode, storage) as plan``."""
+    """Context manager: ``with lease_plan(H, W, psf, mode, storage) as plan``.
+    ``on_new(psf)`` runs before a plan is built for a PSF no pooled plan holds
+    (the batch API's normalisation check: a PSF that matches a pooled plan's
+    bytes has passed it)."""
 
-    def __init__(self, H, W, psf, conv_mode, storage="f64"):
+    def __init__(self, H, W, psf, conv_mode, storage="f64", on_new=None):
         require_gpu()
         self.args = (H, W, psf, conv_mode, storage)
+        self.on_new = on_new
         self.plan = None
 
     def __enter__(self):
@@ -396,6 +400,8 @@ class lease_plan:
             plans = _pool.setdefault(key, [])
             p = next((q for q in plans if not q._leased and _same_psf(q, psf)), None)
             if p is None:
+                if self.on_new is not None and not any(_same_psf(q, psf) for q in plans):
+                    self.on_new(psf)
                 p = _new_plan(H, W, psf, key)
                 p._done = None
                 if len(plans) < _POOL_MAX:

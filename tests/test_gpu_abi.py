@@ -149,6 +149,11 @@ def test_plan_cache_matches_psf_content(sgpmod):
     c = sgpmod.sgp_betaDiv_batch(gn, psf2, 10.0, **kw)
     np.testing.assert_array_equal(b["x"], c["x"])
     assert not np.array_equal(a["x"], b["x"])
+    # the batch API checks a PSF's normalisation when it builds its plan, so an
+    # unnormalised PSF (never pooled) is refused on every call
+    for _ in range(2):
+        with pytest.raises(ValueError, match="PSF is not normalized"):
+            sgpmod.sgp_betaDiv_batch(gn, 2 * psf, 10.0, **kw)
 
 
 def test_device_scope_restores_current_device(sgpmod):
