@@ -688,6 +688,16 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
 #define BSGP_PROJ_GUESS_W 0.3
 #endif
 constexpr double kProjGuessW = BSGP_PROJ_GUESS_W;
+// Teams with few pixels per thread (C2: 8) split the first pass for
+// [lambda_ - dlambda_, lambda_ + dlambda_] instead: the reference's bracketing
+// phase stops there whenever r(0) and r(-/+1) differ in sign (every iteration
+// of the C2 workload, oracle trace), and its secant phase never leaves its
+// bracket, so no evaluation misses; the wider list costs a few entries per
+// thread where each evaluation is one team reduction either way.  (The root
+// moves 2-25x between iterations there, so the +/-30 % guess missed on most.)
+#ifndef BSGP_PROJ_WIDE_PX
+#define BSGP_PROJ_WIDE_PX 16
+#endif
 
 template <class V>
 __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt, Team& tm,
@@ -817,10 +827,11 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
     if (calls == 0) {
       const double lams[3] = {lam, lam - 1.0, lam + 1.0};  // lambda_ -/+ dlambda_ (dlambda_ = 1)
       double Sv[3];
-      const bool guess = isfinite(lam_prev) && lam_prev != 0.0;
+      const bool wide = tm.T > 1 && (long)N <= (long)BSGP_PROJ_WIDE_PX * LS;
+      const bool guess = wide || (isfinite(lam_prev) && lam_prev != 0.0);
       const double w = kProjGuessW * fabs(lam_prev);
       const double slope = pass(std::integral_constant<int, 3>{}, lams, Sv, guess,
-                                lam_prev - w, lam_prev + w);
+                                wide ? lams[1] : lam_prev - w, wide ? lams[2] : lam_prev + w);
       S = Sv[0];
       xl0 = lams[1];
       xs0 = Sv[1];
