@@ -15,6 +15,21 @@
 #include <vector>
 
 #define BSGP_FFT_STATIC_APP 1
+// These plans run two workgroups per CU (their transform buffers and LDS
+// twiddles fill the LDS), so the register budget is that of two waves per
+// SIMD, not the three the other per-wave plans get: 375^2 tiles 97.2 k ->
+// 99.9 k image-it/s (A/B, profiles/r04/ab_round4.txt).  The host sizes the
+// grid from the occupancy the runtime reports, whatever the plan.
+#define BSGP_PERSIST_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+// With that budget the row passes keep two operand batches in flight (the
+// PIPE knobs of bsgp_kernels.hpp): 375^2 +3.1 %, 450^2 +3.8 % (A/B), and
+// the inverse passes issue their first batch before the transform (PRE):
+// +0.9 % / +0.7 %.
+#define BSGP_LS1_PIPE true
+#define BSGP_LSACC_PIPE true
+#define BSGP_BB_PIPE true
+#define BSGP_LS1_PRE true
+#define BSGP_BB_PRE true
 #define bsgp bsgp_app
 #include "bsgp_kernels.hpp"
 
