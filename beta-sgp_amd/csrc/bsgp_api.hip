@@ -402,14 +402,24 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
     }
     // thread groups (bsgp_device.hpp, cooperative passes): as many as the LDS
     // holds, each at least two waves and covering its transform in one load
-    // batch (4 elements per thread).  C4's 2048-point transforms stay on one
-    // group: two groups there measured 6 % slower (A/B); the 400/480-point
-    // grids of the application's subdivisions take four.
-    for (int n = BSGP_COOP_GROUPS; n > 1; n /= 2)
-      if (need(n) <= budget && kCoopBlock / n >= 128 && maxlen <= 4 * (kCoopBlock / n)) {
-        nfw = n;
-        break;
-      }
+    // batch (4 elements per thread); the 400/480-point grids take four.  A
+    // transform too long for that (C4's 2048 points) takes two groups of
+    // 256 threads with two load batches (BSGP_COOP_ELEMS = 8) when the LDS
+    // holds both: each workgroup then runs two row pairs through the same
+    // stages and barriers, and its radix-8 stages use all 512 lanes instead
+    // of 256: C4 k_ls 180 -> 157 us, k_bb 72 -> 68 us, 2114 -> 2221 it/s
+    // (float32 storage; f64 1868 -> 1971), the column kernel staying on one
+    // group (nfc below).
+    const char* ee = getenv("BSGP_COOP_ELEMS");  // (A/B override)
+    const int elems = ee ? atoi(ee) : BSGP_COOP_ELEMS;
+    auto groups = [&](int el) {
+      for (int n = BSGP_COOP_GROUPS; n > 1; n /= 2)
+        if (need(n) <= budget && kCoopBlock / n >= 128 && maxlen <= el * (kCoopBlock / n))
+          return n;
+      return 1;
+    };
+    nfw = groups(4);
+    if (nfw == 1 && elems > 4) nfw = groups(elems);
     p->wg_per_cu = (int)(budget / need(nfw));
     if (p->wg_per_cu > 4) p->wg_per_cu = 4;
     budget = 160 * 1024 / p->wg_per_cu - 256;
@@ -417,8 +427,12 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   g.nfw = nfw;
   // the column kernel of a cooperative plan: BSGP_COOP_COLGROUPS groups (0: as the
   // other kernels), so it may fit more workgroups per CU than they do
-  g.nfc = (g.coop && BSGP_COOP_COLGROUPS > 0 && BSGP_COOP_COLGROUPS < nfw) ? BSGP_COOP_COLGROUPS
-                                                                            : nfw;
+  // (the column kernel keeps one load batch per thread: a 2048-point column per
+  // 256-thread group doubled C4's k_col, 42 -> 75 us, while the row passes gained)
+  int nfc = nfw;
+  while (g.coop && nfc > 1 && maxlen > 4 * (kCoopBlock / nfc)) nfc /= 2;
+  g.nfc = (g.coop && BSGP_COOP_COLGROUPS > 0 && BSGP_COOP_COLGROUPS < nfc) ? BSGP_COOP_COLGROUPS
+                                                                            : nfc;
   p->lds_fft_bytes = (size_t)nfw * 2 * g.lpad * sizeof(cd);
   p->lds_bytes = p->lds_fft_bytes + red_bytes;
   // the per-wave transforms' twiddle tables live in LDS when they fit the same

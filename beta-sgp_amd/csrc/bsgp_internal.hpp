@@ -157,6 +157,9 @@ void persist_kernels_all(std::vector<const void*>& f);
 #ifndef BSGP_COOP_GROUPS
 #define BSGP_COOP_GROUPS 4
 #endif
+#ifndef BSGP_COOP_ELEMS
+#define BSGP_COOP_ELEMS 8  // elements per thread a group may take when one batch leaves one group
+#endif
 #ifndef BSGP_COOP_COLGROUPS
 #define BSGP_COOP_COLGROUPS 0  // 375^2 tiles: k_col on 4 groups 1.49 -> 0.68 ms (A/B)
 #endif
