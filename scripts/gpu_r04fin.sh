@@ -1,0 +1,10 @@
+#!/bin/bash
+# Full GPU suite, then the round-4 evidence (scripts/gpu_r04_evidence.sh).
+set -o pipefail
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf -p no:cacheprovider --timeout 300 \
+  --timeout-method thread > gpurun_out/r04fin_tests.log 2>&1
+rc=$?
+echo "TESTS $rc"; grep -E "FAILED|ERROR" gpurun_out/r04fin_tests.log | head -20; tail -1 gpurun_out/r04fin_tests.log
+[ $rc -eq 0 ] || exit $rc
+bash scripts/gpu_r04_evidence.sh r04fin
