@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-4 evidence from ONE lease: smoke, PMC traffic (two passes) copied to
+# Evidence from ONE lease: smoke, PMC traffic (two passes) copied to
 # profiles/traffic_c3.json, the default bench line (C3) that reads it, the
 # rocprofv3 kernel statistics of the same command, SQ counters of k_persist,
 # and the other configuration lines.  Usage: bash scripts/gpu_r04_evidence.sh TAG
 set -o pipefail
-TAG=${1:-r04e}
+TAG=${1:-ev}
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/$TAG; export TMPDIR=/tmp
 O=gpurun_out/$TAG
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -5 $O/smoke.log; exit 3; }
