@@ -334,12 +334,17 @@ def _same_psf(plan, psf):
         psf.nbytes == 0 or _libc.memcmp(ref.ctypes.data, psf.ctypes.data, psf.nbytes) == 0)
 
 
+# plan-layout overrides read by bsgp_plan_create (A/B knobs): part of the key,
+# so a pooled plan never keeps the layout of an earlier setting
+_PLAN_KNOBS = ("BSGP_PERWAVE_MIN_WG", "BSGP_PERWAVE_TW", "BSGP_COOP_ELEMS")
+
+
 def _plan_key(H, W, psf, conv_mode, storage):
     psf = np.ascontiguousarray(psf, dtype="<f8")
     flat = psf.reshape(-1)
     sample = flat[::max(1, flat.size // 4096)].tobytes()
     return psf, (H, W, psf.shape, hash(sample), conv_mode, storage_code(storage),
-                 torch.cuda.current_device())
+                 torch.cuda.current_device(), tuple(os.environ.get(k) for k in _PLAN_KNOBS))
 
 
 def _new_plan(H, W, psf, key):
@@ -381,16 +386,35 @@ _pool = {}
 _POOL_MAX = 8  # plans kept per key
 
 
-class lease_plan:
-    """Context manager: ``with lease_plan(H, W, psf, mode, storage) as plan``.
-    ``on_new(psf)`` runs before a plan is built for a PSF no pooled plan holds
-    (the batch API's normalisation check: a PSF that matches a pooled plan's
-    bytes has passed it)."""
+_checked = {}  # PSFs that passed a check: (check, dtype, shape, sample hash) -> copy
 
-    def __init__(self, H, W, psf, conv_mode, storage="f64", on_new=None):
+
+def check_psf_once(psf, check):
+    """Run ``check(psf)`` on the caller's own array (its dtype kept: the
+    reference sums the PSF in its own dtype, sgp.py:97-102 / :557-562) unless
+    a byte-identical PSF of the same dtype has passed it before.  Found like
+    the plans: a fingerprint of a strided sample, then memcmp."""
+    psf = np.ascontiguousarray(psf)
+    flat = psf.reshape(-1)
+    key = (check, psf.dtype.str, psf.shape, hash(flat[::max(1, flat.size // 4096)].tobytes()))
+    with _plan_cache_lock:
+        ref = _checked.get(key)
+        if ref is not None and (psf.nbytes == 0 or _libc.memcmp(
+                ref.ctypes.data, psf.ctypes.data, psf.nbytes) == 0):
+            return
+    check(psf)
+    with _plan_cache_lock:
+        if len(_checked) > 32:
+            _checked.clear()
+        _checked[key] = psf.copy()
+
+
+class lease_plan:
+    """Context manager: ``with lease_plan(H, W, psf, mode, storage) as plan``."""
+
+    def __init__(self, H, W, psf, conv_mode, storage="f64"):
         require_gpu()
         self.args = (H, W, psf, conv_mode, storage)
-        self.on_new = on_new
         self.plan = None
 
     def __enter__(self):
@@ -400,8 +424,6 @@ class lease_plan:
             plans = _pool.setdefault(key, [])
             p = next((q for q in plans if not q._leased and _same_psf(q, psf)), None)
             if p is None:
-                if self.on_new is not None and not any(_same_psf(q, psf) for q in plans):
-                    self.on_new(psf)
                 p = _new_plan(H, W, psf, key)
                 p._done = None
                 if len(plans) < _POOL_MAX:

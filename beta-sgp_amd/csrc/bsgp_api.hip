@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cstdlib>
 #include <cmath>
 #include <cstdio>
@@ -25,6 +26,20 @@ thread_local std::string g_err;
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
+}
+
+// A/B override knobs (BSGP_PERWAVE_MIN_WG, BSGP_PERWAVE_TW, BSGP_COOP_ELEMS,
+// BSGP_SPIN_LIMIT): a value that is not a whole decimal number in [lo, hi]
+// is ignored and the compiled default used, so a typo cannot turn into a
+// zero (a spin limit of 0 fails every persistent solve with a timeout).
+long long env_knob(const char* name, long long def, long long lo, long long hi) {
+  const char* e = getenv(name);
+  if (!e || !*e) return def;
+  char* end = nullptr;
+  errno = 0;
+  const long long v = strtoll(e, &end, 10);
+  if (errno != 0 || end == e || *end != '\0' || v < lo || v > hi) return def;
+  return v;
 }
 
 #define HIP_TRY(expr)                                                                  \
@@ -375,10 +390,8 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   // profile), so two workgroups per CU with LDS twiddles can beat three without.
   const size_t twb_all = (size_t)(g.P == g.Q ? g.P : g.P + g.Q) * sizeof(cd);
   {
-    const char* e = getenv("BSGP_PERWAVE_MIN_WG");
-    const int min_wg = e ? atoi(e) : BSGP_PERWAVE_MIN_WG;
-    const char* et = getenv("BSGP_PERWAVE_TW");
-    const size_t tw_need = (et ? atoi(et) : BSGP_PERWAVE_TW) ? twb_all : 0;
+    const int min_wg = (int)env_knob("BSGP_PERWAVE_MIN_WG", BSGP_PERWAVE_MIN_WG, 2, 4);
+    const size_t tw_need = env_knob("BSGP_PERWAVE_TW", BSGP_PERWAVE_TW, 0, 1) ? twb_all : 0;
     for (int wg = 3; wg >= 2 && wg >= min_wg; --wg) {
       const size_t bw = 160 * 1024 / wg - 256;
       if (need(kWaves) > budget && need(kWaves) + tw_need <= bw) {
@@ -410,8 +423,7 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
     // of 256: C4 k_ls 180 -> 157 us, k_bb 72 -> 68 us, 2114 -> 2221 it/s
     // (float32 storage; f64 1868 -> 1971), the column kernel staying on one
     // group (nfc below).
-    const char* ee = getenv("BSGP_COOP_ELEMS");  // (A/B override)
-    const int elems = ee ? atoi(ee) : BSGP_COOP_ELEMS;
+    const int elems = (int)env_knob("BSGP_COOP_ELEMS", BSGP_COOP_ELEMS, 4, 8);  // (A/B override)
     auto groups = [&](int el) {
       for (int n = BSGP_COOP_GROUPS; n > 1; n /= 2)
         if (need(n) <= budget && kCoopBlock / n >= 128 && maxlen <= el * (kCoopBlock / n))
@@ -791,10 +803,7 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   a.pw = p->pw;
   a.storage = p->storage;
   a.spec_off = p->spec_off;
-  {
-    const char* sl = getenv("BSGP_SPIN_LIMIT");
-    a.spin_limit = sl ? (unsigned)strtoul(sl, nullptr, 10) : (1u << 26);
-  }
+  a.spin_limit = (unsigned)env_knob("BSGP_SPIN_LIMIT", 1ll << 26, 0, 0xffffffffll);
   a.ls_cap = (prm->beta > 0.0 && prm->beta < 1.0)
                  ? (int)std::ceil(std::log(1e-12) / std::log(prm->beta)) + 2
                  : 4096;

@@ -518,8 +518,10 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
     if save or errflag:  # sgp()/sgp_betaDiv() keywords: per-image files / err arrays
         raise ValueError("save / errflag are single-image options: use sgp / sgp_betaDiv")
     per_image = (psf.dim() if torch.is_tensor(psf) else np.ndim(psf)) == 3
-    # (a shared PSF is checked when a plan is built for it: lease_plan on_new)
     _B.require_gpu()
+    if not per_image:  # a shared PSF is checked in its own dtype before any upload
+        psf = np.asarray(psf.cpu().numpy() if torch.is_tensor(psf) else psf)
+        _B.check_psf_once(psf, _check_psf)
     # float32 images (the application's FITS data): the reference's float32
     # prelude on the device, per image (include/bsgp.h gn_f32, ABI 3)
     if gn_f32 is None:
@@ -574,8 +576,7 @@ def _solve_batch(variant, gns, psf, bkgs, betaParams=None, flux=None, init_recon
         plan = _B.per_image_plan(H, W, psf, mode, storage=storage)
         out = plan.solve(gns, bkgs, prm, flux=fl, x0=x0, beta0=b0, profile=profile)
     else:
-        with _B.lease_plan(H, W, np.asarray(psf), mode, storage=storage,
-                           on_new=_check_psf) as plan:
+        with _B.lease_plan(H, W, psf, mode, storage=storage) as plan:
             out = plan.solve(gns, bkgs, prm, flux=fl, x0=x0, beta0=b0, profile=profile)
     if device_out:
         return out

@@ -126,3 +126,38 @@ def test_check_status_raises_on_status_bits():
     with pytest.raises(ValueError, match="zero-size array"):
         _bsgp.check_status(c)
     assert _bsgp.BSGP_ERR_HIP == -2 and _bsgp.BSGP_ERR_ARG == -1
+
+
+def _f32_psf_sum_exact(seed):
+    """A float32 PSF normalised in float32 whose float32 sum is exactly 1 while
+    its float64 sum is not within the reference's 1e4*eps."""
+    rng = np.random.default_rng(seed)
+    for _ in range(200):
+        p = rng.random((25, 25), dtype=np.float32)
+        p = (p / np.sum(p)).astype(np.float32)
+        if np.sum(p) == np.float32(1) and abs(np.sum(p.astype(np.float64)) - 1) > 1e4 * np.finfo(float).eps:
+            return p
+    pytest.skip("no such PSF found")
+
+
+def test_shared_psf_checked_in_its_own_dtype():
+    """The batch API checks a shared PSF as the reference does (sgp.py:97-102:
+    np.sum in the PSF's own dtype), on the caller's array, once per content."""
+    import _bsgp
+    import sgp
+    p = _f32_psf_sum_exact(0)
+    calls = []
+
+    def check(a):
+        calls.append(a.dtype)
+        sgp._check_psf(a)
+
+    _bsgp.check_psf_once(p, check)        # float32 sum == 1: accepted
+    _bsgp.check_psf_once(p.copy(), check)  # same bytes, same dtype: not re-run
+    assert calls == [np.float32]
+    with pytest.raises(ValueError, match="not normalized"):  # the float64 sum is off by >2e-12
+        _bsgp.check_psf_once(p.astype(np.float64), check)
+    bad = p.copy()
+    bad[0, 0] += np.float32(1e-3)
+    with pytest.raises(ValueError, match="not normalized"):
+        _bsgp.check_psf_once(bad, check)

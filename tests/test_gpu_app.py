@@ -65,8 +65,11 @@ def test_crowded_full_frame_matches_reference(sgpmod, monkeypatch):
     44-50, 84-115): the whole 450x450 float32 frame on its 480-point grid, a
     background map, the published flux, beta-SGP from the published best
     initial beta and the KL branch (stop rule 3, tol 1e-5): the single-image
-    drop-in (automatic team) and a one-workgroup batch of both frames (the
-    cooperative plans' persistent solver) against the reference's runs."""
+    drop-in (automatic team) and a one-workgroup batch of both frames against
+    the reference's runs.  The 480-point grid is a per-wave plan at two
+    workgroups per CU (BSGP_PERWAVE_MIN_WG 2), so the batch runs the
+    application build's persistent solver (bsgp_persist_app.hip); the
+    cooperative persistent build is covered by test_gpu_persist's 640^2 frame."""
     from conftest import crowded_case
     for name in ("crowded_beta", "crowded_kl"):
         gn, psf, bkg, kw, fn, fx = crowded_case(name)
@@ -364,3 +367,24 @@ def test_no_positive_scaling_bound_raises_like_reference(sgpmod, persistent):
     for i in (0, 2):
         assert iters[i] == one["iters"][0] and cnt[i, 3] == 0
         np.testing.assert_array_equal(out["x"][i].cpu().numpy(), one["x"][0])
+
+
+def test_float32_psf_accepted_by_batch_like_dropin(sgpmod):
+    """A float32 PSF normalised in float32 (float32 sum exactly 1, float64 sum
+    off by more than 1e4*eps) passes the reference's check (sgp.py:97-102 sums
+    in the PSF's dtype): the single-image drop-in and the batch API accept it
+    alike and give the same bits (the batch had summed a float64
+    copy and refused it)."""
+    from test_abi import _f32_psf_sum_exact
+    fx = golden("ref_lin64_beta.npz")
+    kw = ref_kwargs(fx)
+    kw.update(MAXIT=8)
+    gn = fx["gn"].astype(np.float64)
+    p = _f32_psf_sum_exact(1)
+    x, it, _, _, _ = sgpmod.sgp_betaDiv(gn, p, np.float64(100.0), **kw)
+    b = kw.pop("betaParam")
+    out = sgpmod.sgp_betaDiv_batch(gn[None], p, 100.0, betaParams=[b], team=1, **kw)
+    assert int(out["iters"][0]) == it
+    np.testing.assert_array_equal(out["x"][0], x)
+    with pytest.raises(ValueError, match="not normalized"):
+        sgpmod.sgp_betaDiv_batch(gn[None], p.astype(np.float64), 100.0, betaParams=[b], **kw)

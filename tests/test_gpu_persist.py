@@ -143,3 +143,34 @@ def test_persistent_cooperative_plans_bitwise(sgpmod, case):
     extra = dict(adapt_beta=case == "adapt", storage="f32" if case == "f32storage" else "f64")
     both(sgpmod.sgp_betaDiv_batch, gns, psf, bk, flux=flux, betaParams=[b0, 1.02, 0.97], **kw,
          **extra)
+
+
+@pytest.mark.parametrize("case", ["beta", "kl"])
+def test_persistent_app_build_375_within_rounding(sgpmod, case):
+    """The application's 375^2 tiles (400-point grid, per-wave plan) run the
+    application build's persistent solver (bsgp_persist_app.hip), whose
+    400-point transforms use the compile-time 8*10*5 plan; the phase kernels
+    keep the runtime 4*4*5*5 plan, which rounds differently.  So the two paths
+    agree to rounding, not bitwise: equal iteration counts, x and the
+    discrepancies at rtol 1e-9."""
+    from conftest import app_case
+    gn, psf, bkg, kw, fn, fx = app_case("app_beta2" if case == "beta" else "app_kl")
+    assert gn.shape == (375, 375)
+    kw = dict(kw)
+    flux = kw.pop("flux")
+    kw.update(MAXIT=12, stop_criterion=1, team=1)
+    gns = np.stack([gn, np.roll(gn, 17, 0), np.roll(gn, 9, 1)])
+    if case == "beta":
+        b0 = kw.pop("betaParam")
+        fn2, extra = sgpmod.sgp_betaDiv_batch, dict(betaParams=[b0, 1.02, 0.97])
+    else:
+        fn2, extra = sgpmod.sgp_batch, {}
+    p0 = fn2(gns, psf, bkg, flux=flux, persistent=0, **kw, **extra)
+    p1 = fn2(gns, psf, bkg, flux=flux, persistent=1, **kw, **extra)
+    np.testing.assert_array_equal(p1["iters"], p0["iters"])
+    assert np.all(p1["counters"][:, 3] == 0)
+    for i in range(3):
+        r = np.linalg.norm(p1["x"][i] - p0["x"][i]) / np.linalg.norm(p0["x"][i])
+        assert r < 1e-9, (i, r)
+        n = int(p0["iters"][i]) + 1
+        np.testing.assert_allclose(p1["discr"][i, :n], p0["discr"][i, :n], rtol=1e-9)
