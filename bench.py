@@ -102,8 +102,15 @@ CONFIGS = {
                      desc="{B} float32 31x31 star stamps (cutouts of results/SUBDIV_ORIGIMG.fits "
                           "at bright pixels) x the application's 5 seeds, DIAPL 31x31 PSF, "
                           "circular A"),
+    # the same stamps through the application's KL branch (USE_BETADIV False,
+    # application_sgp_star_stamps.py:107-112): sgp(...), stop rule 3, no seeds
+    "stamps31_kl": dict(n=31, k=31, nstars=0, batch=16384, circular=True, stamps=True, kl=True,
+                        maxit=500,
+                        desc="{B} float32 31x31 star stamps (cutouts of results/SUBDIV_ORIGIMG.fits "
+                             "at bright pixels), KL SGP, DIAPL 31x31 PSF, circular A"),
 }
 STAMP_PUBLISHED = 1167.5  # it/s, beta-SGP star stamps (results/EXEC_TIME_BETA.npy, NUM_ITERS_BETA.npy)
+STAMP_KL_PUBLISHED = 1436.7  # it/s, KL star stamps (results/EXEC_TIME.npy, NUM_ITERS.npy)
 # the reference's own published single-frame rates for the subdivision application (context
 # only: one image on unstated hardware, so vs_baseline stays null for these lines)
 PUBLISHED_CONTEXT = {
@@ -158,12 +165,15 @@ def stamp_inputs(B, seed=0):
     return cuts, np.asarray(psf, dtype=np.float64), bkg, flux, np.resize(np.asarray(betas), B)
 
 
-def stamp_kwargs(maxit):
-    """application_sgp_star_stamps.py:82-90 (DEFAULT_PARAMS unpacked, sgp.py:34)."""
-    return dict(gamma=1e-4, beta=0.4, alpha_min=1e-5, alpha_max=1e5, alpha=10.0, M_alpha=3,
-                tau=0.5, M=1, proj_type=1, max_projs=1000, init_recon=2, stop_criterion=3,
-                MAXIT=maxit, ccd_sat_level=65000, scale_data=True, lr=1e-3, lr_exp_param=0.1,
-                schedule_lr=True, adapt_beta=True, use_original_SGP_Afunction=True)
+def stamp_kwargs(maxit, kl=False):
+    """application_sgp_star_stamps.py:82-90 (DEFAULT_PARAMS unpacked, sgp.py:34);
+    kl: the sgp(...) call of its KL branch (:107-112), no beta keywords."""
+    kw = dict(gamma=1e-4, beta=0.4, alpha_min=1e-5, alpha_max=1e5, alpha=10.0, M_alpha=3,
+              tau=0.5, M=1, proj_type=1, max_projs=1000, init_recon=2, stop_criterion=3,
+              MAXIT=maxit, ccd_sat_level=65000, scale_data=True, use_original_SGP_Afunction=True)
+    if not kl:
+        kw.update(lr=1e-3, lr_exp_param=0.1, schedule_lr=True, adapt_beta=True)
+    return kw
 
 
 def synth_batch(B, n, k, nstars, seed0, bkg=100.0, circular=False):
@@ -234,20 +244,20 @@ def cpu_baseline(n, k, nstars, images, maxit, workers, circular=False):
                       f"({iters / cpu_s:.1f} image-it/s per core)"}
 
 
-def cpu_baseline_stamps(kw, images, workers):
+def cpu_baseline_stamps(kw, images, workers, kl=False):
     """The oracle on `images` stamps of the same stamp workload, one stamp per
     task on `workers` processes."""
     import cpu_bench
     cuts, psf, bk, fl, betas = stamp_inputs(images, seed=777)
-    okw = {k_: v for k_, v in kw.items() if k_ in stamp_kwargs(1)}
-    jobs = [(cuts[i], psf, float(bk[i]), float(fl[i]), float(betas[i]), okw)
+    okw = {k_: v for k_, v in kw.items() if k_ in stamp_kwargs(1, kl)}
+    jobs = [(cuts[i], psf, float(bk[i]), float(fl[i]), None if kl else float(betas[i]), okw)
             for i in range(images)]
     iters, wall, cpu_s = cpu_bench.run_pool_jobs(jobs, workers)
     ncpu = os.cpu_count() or 1
     return {"value": iters / wall, "unit": "image-iterations/s", "cores": workers,
             "kind": "port", "cpu_model": cpu_model(), "host_cpus": ncpu,
-            "sample": f"{images} float32 31x31 stamps of the same workload (adaptive beta, "
-                      f"stop 3) with oracle/sgp_oracle.py, one stamp per process on {workers} "
+            "sample": f"{images} float32 31x31 stamps of the same workload "
+                      f"({'KL' if kl else 'adaptive beta'}, stop 3) with oracle/sgp_oracle.py, one stamp per process on {workers} "
                       f"processes ({cpu_model()}): {iters} image-iterations in {wall:.1f}s wall "
                       f"({iters / cpu_s:.1f} image-it/s per core)"}
 
@@ -319,6 +329,124 @@ def launch_ranks(n, argv, poll_s=0.2):
     return 0
 
 
+APP_PUBLISHED = 6.42  # it/s: the reference's one 375x375 subdivision, beta-SGP (SUBDIV_EXEC_TIME_BETA.npy)
+
+
+def app375_inputs():
+    """The application's own call (application_sgp_subdivisions.py:69-107): the
+    375x375 big-endian float32 subdivision results/SUBDIV_ORIGIMG.fits as
+    fits.getdata returns it, the >f8 31x31 DIAPL PSF, a per-pixel background
+    map (photutils' Background2D is absent: the smoothed-median map of
+    tests/golden/make_golden.py app) and the flux, with the application's
+    keyword arguments (linear A, projection, stop rule 3 at tol 1e-5, fixed
+    beta) and its five seeds.  Host arrays, from tests/golden (the copies
+    the GPU box has)."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "app_subdiv_inputs.npz"))
+    kw = dict(gamma=1e-4, beta=0.4, alpha_min=1e-5, alpha_max=1e5, alpha=10.0, M_alpha=3,
+              tau=0.5, M=1, proj_type=1, max_projs=1000, init_recon=2, stop_criterion=3,
+              save=False, verbose=True, ccd_sat_level=65000, scale_data=True, lr=1e-3,
+              lr_exp_param=0.1, schedule_lr=True, adapt_beta=False,
+              use_original_SGP_Afunction=False, tol_convergence=1e-5,
+              flux=np.float64(z["flux"]))
+    return z["img"], z["psf"], z["bkg"], kw, [float(b) for b in z["betas"]]
+
+
+def bench_app375(args):
+    """--config app375: the drop-in at the application's real call shape, one
+    subdivision at a time, end to end from host arrays (the application's own
+    timing covers one sgp_betaDiv call, SUBDIV_EXEC_TIME_BETA.npy):
+    (a) value: sgp_betaDiv on the one image (seed 0), iterations / wall s;
+    (b) multistart: sgp_betaDiv_multistart, the five seed candidates as one
+        batched launch (the application's five calls + its final re-solve,
+        which repeats the best candidate's run and is returned without
+        solving again), candidate iterations / wall s;
+    with the GPU span of the solve (HIP events) beside the wall, the oracle
+    (a port of the reference) timed on the same call on one host core, and
+    the reference's published 6.42 it/s as context."""
+    import contextlib
+    import io
+    import sgp
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    img, psf, bkg, kw, betas = app375_inputs()
+    quiet = contextlib.redirect_stdout(io.StringIO())  # the drop-in prints as the reference does
+    quiet.__enter__()
+    kw1 = dict(kw, betaParam=betas[0])
+    for _ in range(max(1, args.warmup)):
+        sgp.sgp_betaDiv(img, psf, bkg, **kw1)
+        sgp.sgp_betaDiv_multistart(img, psf, bkg, betas=betas, **kw)
+    torch.cuda.synchronize()
+
+    def timed(fn):
+        walls, spans, its = [], [], []
+        for _ in range(args.steps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record()
+            r = fn()
+            e1.record()
+            torch.cuda.synchronize()
+            walls.append(time.perf_counter() - t0)
+            spans.append(e0.elapsed_time(e1) * 1e-3)
+            its.append(r)
+        return float(np.median(walls)), float(np.median(spans)), its[-1]
+
+    w1, g1, it1 = timed(lambda: sgp.sgp_betaDiv(img, psf, bkg, **kw1)[1])
+
+    def ms():
+        _, info = sgp.sgp_betaDiv_multistart(img, psf, bkg, betas=betas, **kw)
+        return sum(c[1] for c in info["candidates"])
+    wm, gm, itm = timed(ms)
+    res = {
+        "metric": "SGP iterations/sec (fp64) of the drop-in on one 375x375 float32 subdivision "
+                  "(the application's call shape)",
+        "value": it1 / w1, "unit": "iterations/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": w1 * 1e3, "higher_is_better": True,
+        "scaling": "none (one image: latency-bound)", "vs_baseline": None,
+        "dtype": "f64 (the reference's float32 prelude on float32 data)",
+        "data": "the reference's results/SUBDIV_ORIGIMG.fits (>f4, tests/golden copy), its DIAPL "
+                "PSF, a smoothed-median background map, flux from the published restored image",
+        "config": {"workload": "APP375: application_sgp_subdivisions.py:84-91 on one 375x375 "
+                               "subdivision: sgp_betaDiv, linear A (400-point grid), proj_type=1, "
+                               "init_recon=2, stop_criterion=3 (tol 1e-5), beta fixed (seed 0)",
+                   "iterations": int(it1), "gpu_span_ms": g1 * 1e3,
+                   "host_share": 1.0 - g1 / w1},
+        "multistart": {"what": "sgp_betaDiv_multistart: the five seeds as one batched launch",
+                       "candidate_iterations": int(itm), "ms": wm * 1e3, "gpu_span_ms": gm * 1e3,
+                       "value": itm / wm, "unit": "candidate iterations/s"},
+        "context": PUBLISHED_CONTEXT["sub375"],
+        "roofline": None, "cpu_baseline": None,
+    }
+    if not args.no_profile:
+        import _bsgp
+        g = torch.from_numpy(np.asarray(img, dtype=np.float32).copy()).cuda()[None]
+        b = torch.from_numpy(np.asarray(bkg, dtype=np.float64)).cuda()[None]
+        bk = {k_: v for k_, v in kw.items() if k_ not in ("save", "verbose", "flux")}
+        prof = sgp.sgp_betaDiv_batch(g, psf, b, betaParams=[betas[0]], profile=True,
+                                     flux=np.array([kw["flux"]]), **bk)
+        names = ["k_setup", "k_dir", "k_col", "k_ls", "k_bb", "k_persist"]
+        kms, nl = prof["kernel_ms"], prof["launches"]
+        it = int(prof["iters"][0])
+        res["roofline"] = {
+            "note": "one image is latency-bound: per-kernel spans of the profiled solve (one "
+                    "stream, HIP events around every launch); bytes per iteration ~ 245 B/px "
+                    "x 375^2 = 34 MB, i.e. ~5 us of HBM time against the span below",
+            "team": int(prof["counters"][0, 5]), "iterations": it,
+            "us_per_iteration": {n_: float(kms[i] / max(it, 1) * 1e3) for i, n_ in enumerate(names)
+                                 if i > 0 and nl[i] > 0},
+            "profiled_solve_ms": float(np.sum(kms))}
+    if not args.no_cpu:
+        import sgp_oracle
+        t0 = time.perf_counter()
+        _, ito, _, _, _ = sgp_oracle.sgp_betaDiv(img, psf, bkg, **kw1)
+        el = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": ito / el, "unit": "iterations/s", "cores": 1,
+                               "kind": "port", "cpu_model": cpu_model(),
+                               "sample": f"the same call with oracle/sgp_oracle.py on one core: "
+                                         f"{ito} iterations in {el:.2f} s"}
+    quiet.__exit__(None, None, None)
+    print(json.dumps(res), flush=True)
+
+
 def kernel_bytes(H, W, P, Qh, counters, iters, beta, series, compact, bmap, fused_at_col,
                  vb=8.0):
     """Algorithmic HBM bytes of each kernel class over one solve: the passes
@@ -369,7 +497,7 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS) + ["app375"])
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (c2/c3/c4)")
     ap.add_argument("--maxit", type=int, default=None, help="default 100 (500 for stamps31)")
     ap.add_argument("--ls-spec", type=int, default=None)
@@ -413,6 +541,8 @@ def main():
     global torch
     import torch as _torch
     torch = _torch
+    if args.config == "app375":
+        return bench_app375(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -433,6 +563,7 @@ def main():
     cfg = CONFIGS[args.config]
     n, k, nstars, circ = cfg["n"], cfg["k"], cfg["nstars"], cfg["circular"]
     stamps = cfg.get("stamps", False)
+    kl = cfg.get("kl", False)
     if args.maxit is None:
         args.maxit = cfg.get("maxit", 100)
     strong = "total" in cfg
@@ -446,7 +577,7 @@ def main():
                       proj_cache=args.proj_cache, storage=args.storage,
                       persistent=args.persistent, stop3=args.stop3)
     if stamps:
-        kw = dict(stamp_kwargs(args.maxit), ls_spec=args.ls_spec, streams=args.streams,
+        kw = dict(stamp_kwargs(args.maxit, kl), ls_spec=args.ls_spec, streams=args.streams,
                   team=args.team, proj_cache=args.proj_cache, storage=args.storage,
                   persistent=args.persistent)
 
@@ -466,7 +597,7 @@ def main():
             gn = torch.from_numpy(cuts).cuda()  # float32: the reference's float32 arithmetic
             bkg = torch.from_numpy(bk_h).cuda()
             flux = torch.from_numpy(fl_h).cuda()
-            extra = dict(betaParams=betas, flux=flux)
+            extra = dict(flux=flux) if kl else dict(betaParams=betas, flux=flux)
         else:
             gn, psf = synth_batch(B, n, k, nstars, seed0=seed0, circular=circ)
             bkg = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
@@ -474,8 +605,10 @@ def main():
         kw.update(extra)
         torch.cuda.synchronize()
 
+        solve = sgp.sgp_batch if kl else sgp.sgp_betaDiv_batch
+
         def step():
-            return sgp.sgp_betaDiv_batch(gn, psf, bkg, device_out=True, **kw)
+            return solve(gn, psf, bkg, device_out=True, **kw)
 
         def sync():
             torch.cuda.synchronize()
@@ -513,8 +646,9 @@ def main():
         return
 
     if stamps:
-        workload = (f"STAMPS31: " + cfg["desc"].format(B=B) + f", adaptive beta-SGP, proj_type=1, "
-                    f"init_recon=2, MAXIT={args.maxit}, stop_criterion=3 (tol 1e-4)")
+        workload = (f"{args.config.upper()}: " + cfg["desc"].format(B=B)
+                    + (", KL SGP" if kl else ", adaptive beta-SGP")
+                    + f", proj_type=1, init_recon=2, MAXIT={args.maxit}, stop_criterion=3 (tol 1e-4)")
     else:
         workload = (f"{args.config.upper()}: "
                     + cfg["desc"].format(n=n, B=B, T=cfg.get("total", B))
@@ -531,13 +665,15 @@ def main():
         "ms_per_step": elapsed_max / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
-        "vs_baseline": (value / STAMP_PUBLISHED) if stamps else None,
+        "vs_baseline": (value / (STAMP_KL_PUBLISHED if kl else STAMP_PUBLISHED)) if stamps else None,
         "dtype": "f64" if args.storage == "f64" else "f32 storage, f64 arithmetic",
         "data": ("the reference's float32 frame results/SUBDIV_ORIGIMG.fits cut into 31x31 "
                  "stamps around its brightest pixels (tests/golden copy), its DIAPL PSF; "
-                 "vs_baseline = value / 1167.5 it/s, the reference's published star-stamp "
-                 "beta-SGP rate (results/EXEC_TIME_BETA.npy, NUM_ITERS_BETA.npy; hardware "
-                 "unstated)") if stamps else
+                 + ("vs_baseline = value / 1436.7 it/s, the reference's published star-stamp "
+                    "KL rate (results/EXEC_TIME.npy, NUM_ITERS.npy; hardware unstated)" if kl else
+                    "vs_baseline = value / 1167.5 it/s, the reference's published star-stamp "
+                    "beta-SGP rate (results/EXEC_TIME_BETA.npy, NUM_ITERS_BETA.npy; hardware "
+                    "unstated)")) if stamps else
                 "synthetic (SURVEY §8d generator: pareto point sources * 25x25 Gaussian PSF "
                 "+ Poisson, bkg 100), built on device",
         "config": {"workload": workload, "images_per_gpu": B,
@@ -558,14 +694,18 @@ def main():
     import sgp
     cnt = out["counters"].cpu().numpy()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    persistent = kw["persistent"] if kw["persistent"] is not None else sgp.PERSIST_DEFAULT
+    one_wg = int(cnt[0, 5]) == 1
     result["config"].update({"ls_spec": kw["ls_spec"] or sgp.LS_SPEC_DEFAULT,
-                             "streams": kw["streams"] or sgp.STREAMS_DEFAULT,
+                             # sub-batches actually run: the persistent solver of
+                             # one-workgroup images runs the batch as one (bsgp_api.hip)
+                             "streams": 1 if (persistent and one_wg) else
+                             (kw["streams"] or sgp.STREAMS_DEFAULT),
                              "team": int(cnt[0, 5]),
                              "proj_cache": kw["proj_cache"] if kw["proj_cache"] is not None
                              else sgp.PROJ_CACHE_DEFAULT,
                              "gn_compact": sgp.GN_COMPACT_DEFAULT, "storage": args.storage,
-                             "persistent": kw["persistent"] if kw["persistent"] is not None
-                             else sgp.PERSIST_DEFAULT,
+                             "persistent": persistent,
                              "stop_criterion": kw["stop_criterion"]})
     if not args.no_profile:
         result["roofline"] = roofline(args, kw, gn, psf, bkg, B, n, kern_ms)
@@ -577,7 +717,7 @@ def main():
         cpu_maxit = args.cpu_maxit if args.cpu_maxit else args.maxit
         if stamps:
             result["cpu_baseline"] = cpu_baseline_stamps(kw, args.cpu_images * 8,
-                                                         min(workers, args.cpu_images * 8))
+                                                         min(workers, args.cpu_images * 8), kl)
         else:
             result["cpu_baseline"] = cpu_baseline(n, k, nstars, images, cpu_maxit,
                                                   min(workers, images), circular=circ)
@@ -594,7 +734,9 @@ def end_to_end(kw, gn, psf, bkg):
     b_host = bkg.cpu().numpy()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    out = sgp.sgp_betaDiv_batch(g_host, psf, b_host, **kw)
+    kl = "betaParams" not in kw and "adapt_beta" not in kw
+    host_kw = {k_: (v.cpu().numpy() if torch.is_tensor(v) else v) for k_, v in kw.items()}
+    out = (sgp.sgp_batch if kl else sgp.sgp_betaDiv_batch)(g_host, psf, b_host, **host_kw)
     el = time.perf_counter() - t0
     its = float(np.sum(out["iters"]))
     h2d = g_host.nbytes + b_host.nbytes
@@ -611,13 +753,14 @@ def profile_kernels(kw, gn, psf, bkg, n):
     launch that runs every phase of every iteration: its bytes are all of them."""
     import _bsgp
     import sgp
-    prof = sgp.sgp_betaDiv_batch(gn, psf, bkg, profile=True, **kw)
+    kl = "betaParams" not in kw and "adapt_beta" not in kw
+    prof = (sgp.sgp_batch if kl else sgp.sgp_betaDiv_batch)(gn, psf, bkg, profile=True, **kw)
     plan = _bsgp.get_plan(n, n, psf, _bsgp.BSGP_CONV_CIRCULAR if kw["use_original_SGP_Afunction"]
                           else _bsgp.BSGP_CONV_LINEAR_FILL, storage=kw["storage"])
     cnt, iters = prof["counters"], prof["iters"]
     team = int(cnt[0, 5])
-    kb = kernel_bytes(n, n, plan.P, plan.Q // 2 + 1, cnt, iters, beta=True,
-                      series=not kw.get("adapt_beta", False),
+    kb = kernel_bytes(n, n, plan.P, plan.Q // 2 + 1, cnt, iters, beta=not kl,
+                      series=not kl and not kw.get("adapt_beta", False),
                       compact=sgp.GN_COMPACT_DEFAULT == 1, bmap=False,
                       fused_at_col=(team == 1), vb=4.0 if kw["storage"] == "f32" else 8.0)
     kb["k_persist"] = float(sum(kb.values()))
@@ -645,16 +788,19 @@ def roofline(args, kw, gn, psf, bkg, B, n, solve_ms):
     dom = max(names, key=lambda k_: kernels[k_]["ms_total"])
     d = kernels[dom]
     traffic = load_traffic(args.config)
-    tr = None
+    tr, tr_src = None, None
     if traffic and isinstance(traffic.get("kernels"), dict) and dom in traffic["kernels"]:
         tr = traffic["kernels"][dom].get("bytes_per_launch")
+        # not measured in this run: read from the committed PMC record
+        tr_src = (f"profiles/traffic_{args.config}.json (committed PMC record, not this run): "
+                  + str(traffic.get("note", "")))
     if dom == "k_persist":
         unit = (f"one launch = the whole solve: {B} images x {int(iters.max())} iterations, "
                 f"every phase (persistent task-queue kernel)")
     else:
         unit = f"one launch = {B} images x one iteration of {dom} (profiled solve on one stream)"
     out = {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS,
-           "unit": "GB/s", "frac": d["frac"], "traffic": tr,
+           "unit": "GB/s", "frac": d["frac"], "traffic": tr, "traffic_source": tr_src,
            "ms_per_launch": d["ms_per_launch"], "bytes_per_launch": d["bytes_per_launch"],
            "launch_unit": unit, "kernels": kernels, "profiled_solve_ms": prof_total,
            "solve": {"alg_bytes": alg_total, "ms_timed": solve_ms,

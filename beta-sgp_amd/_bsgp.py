@@ -105,6 +105,8 @@ def lib():
             L.bsgp_abi_version.restype = i32
             L.bsgp_plan_create.argtypes = [i32, i32, vp, i32, i32, i32, i32, i32,
                                            ctypes.POINTER(vp)]
+            L.bsgp_plan_create_checked.argtypes = [i32, i32, vp, i32, i32, i32, i32, i32, i32,
+                                                   ctypes.POINTER(vp)]
             L.bsgp_plan_destroy.argtypes = [vp]
             L.bsgp_plan_info.argtypes = [vp, vp, vp, vp, vp]
             L.bsgp_solve_device.argtypes = [vp, i32, vp, vp, vp, vp]
@@ -121,7 +123,7 @@ def lib():
             L.bsgp_fits_to_f64.argtypes = [vp, i64, i32, dbl, dbl, vp, vp]
             L.bsgp_psf_stamps.argtypes = [ctypes.POINTER(PsfModel), vp, i32, i32, i32, vp, vp]
             L.bsgp_plan_set_psfs.argtypes = [vp, vp, i32, vp]
-            for name in ["bsgp_plan_create", "bsgp_plan_destroy", "bsgp_plan_info",
+            for name in ["bsgp_plan_create", "bsgp_plan_create_checked", "bsgp_plan_destroy", "bsgp_plan_info",
                          "bsgp_solve_device", "bsgp_solve_host", "bsgp_solve_profiled",
                          "bsgp_apply_operator",
                          "bsgp_project_df", "bsgp_beta_div", "bsgp_beta_div_deriv",
@@ -136,7 +138,7 @@ def lib():
     return _lib
 
 
-EXPORTED = ["bsgp_plan_create", "bsgp_plan_destroy", "bsgp_plan_info", "bsgp_solve_device",
+EXPORTED = ["bsgp_plan_create", "bsgp_plan_create_checked", "bsgp_plan_destroy", "bsgp_plan_info", "bsgp_solve_device",
             "bsgp_solve_host", "bsgp_solve_profiled", "bsgp_apply_operator", "bsgp_project_df", "bsgp_beta_div",
             "bsgp_beta_div_deriv", "bsgp_beta_div_grad_parts", "bsgp_device_synchronize",
             "bsgp_last_error", "bsgp_abi_version", "bsgp_extract_tiles", "bsgp_coadd_tiles",
@@ -179,8 +181,11 @@ class Plan:
         self.device = device
         self.storage = storage
         h = ctypes.c_void_p()
-        rc = lib().bsgp_plan_create(self.H, self.W, psf.ctypes.data, self.kh, self.kw, conv_mode,
-                                    storage, device, ctypes.byref(h))
+        # the drop-in checks the PSF's normalisation itself, in the caller's
+        # dtype (sgp._check_psf, check_psf_once; per-image PSFs in
+        # bsgp_plan_set_psfs), so the library's float64 check is skipped
+        rc = lib().bsgp_plan_create_checked(self.H, self.W, psf.ctypes.data, self.kh, self.kw,
+                                            conv_mode, storage, device, 1, ctypes.byref(h))
         if rc != 0:
             raise BsgpError(rc, lib().bsgp_last_error().decode(errors="replace"))
         self.h = h

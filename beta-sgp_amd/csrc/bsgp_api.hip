@@ -321,6 +321,12 @@ int bsgp_device_synchronize(void) {
 
 int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_t kw,
                      int32_t conv_mode, int32_t storage, int32_t device, bsgp_plan* out) {
+  return bsgp_plan_create_checked(H, W, psf, kh, kw, conv_mode, storage, device, 0, out);
+}
+
+int bsgp_plan_create_checked(int32_t H, int32_t W, const double* psf, int32_t kh, int32_t kw,
+                             int32_t conv_mode, int32_t storage, int32_t device,
+                             int32_t psf_checked, bsgp_plan* out) {
   if (!out) return fail(BSGP_ERR_ARG, "out is NULL");
   if (storage != BSGP_STORAGE_F64 && storage != BSGP_STORAGE_F32)
     return fail(BSGP_ERR_ARG, "bad storage");
@@ -331,8 +337,9 @@ int bsgp_plan_create(int32_t H, int32_t W, const double* psf, int32_t kh, int32_
   if (conv_mode == BSGP_CONV_CIRCULAR && (kh != H || kw != W))
     return fail(BSGP_ERR_ARG,
                 "circular A (use_original_SGP_Afunction=True) needs psf.shape == gn.shape");
-  // PSF normalisation check (sgp.py:97-102)
-  {
+  // PSF normalisation check (sgp.py:97-102), unless the caller has made it in
+  // the PSF's own dtype (a float32 PSF sums to 1 in float32, not in float64)
+  if (!psf_checked) {
     double s = 0;
     for (int i = 0; i < kh * kw; ++i) s += psf[i];
     if (std::fabs(s - 1.0) > 1e4 * 2.220446049250313e-16) {

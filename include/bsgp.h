@@ -171,6 +171,14 @@ typedef struct {
  * scalar in float64; SURVEY config C4).  Synchronous. */
 int bsgp_plan_create(int32_t H, int32_t W, const double* psf_host, int32_t kh, int32_t kw,
                      int32_t conv_mode, int32_t storage, int32_t device, bsgp_plan* out);
+/* The same; psf_checked != 0 skips the normalisation check because the caller
+ * has applied the reference's check (sgp.py:97-102 / 557-562: np.sum in the
+ * PSF's OWN dtype) before widening the PSF to float64 -- a float32 PSF whose
+ * float32 sum is 1 has a float64 sum off by up to ~1e-7, which the float64
+ * check here would refuse.  The Python drop-in always checks first. */
+int bsgp_plan_create_checked(int32_t H, int32_t W, const double* psf_host, int32_t kh,
+                             int32_t kw, int32_t conv_mode, int32_t storage, int32_t device,
+                             int32_t psf_checked, bsgp_plan* out);
 int bsgp_plan_destroy(bsgp_plan plan);
 /* FFT grid (P x Q) and the per-slot workspace bytes of the plan. */
 int bsgp_plan_info(bsgp_plan plan, int32_t* P, int32_t* Q, int64_t* slot_bytes,

@@ -74,13 +74,16 @@ def run_pool(n, k, nstars, images, kw, workers):
 
 
 def solve_job(args):
-    """One star-stamp solve with the oracle (bench.py stamps31): (cutout,
-    psf, bkg, flux, beta, kwargs) -> (iters, seconds)."""
+    """One star-stamp solve with the oracle (bench.py stamps31 / stamps31_kl):
+    (cutout, psf, bkg, flux, beta or None for KL, kwargs) -> (iters, seconds)."""
     cut, psf, bkg, flux, beta, kw = args
     import sgp_oracle
     t = time.perf_counter()
-    _, it, _, _, _ = sgp_oracle.sgp_betaDiv(cut, psf, np.float64(bkg), flux=np.float64(flux),
-                                            betaParam=beta, **kw)
+    if beta is None:  # the KL branch (application_sgp_star_stamps.py:107-112)
+        _, it, _, _, _ = sgp_oracle.sgp(cut, psf, np.float64(bkg), flux=np.float64(flux), **kw)
+    else:
+        _, it, _, _, _ = sgp_oracle.sgp_betaDiv(cut, psf, np.float64(bkg), flux=np.float64(flux),
+                                                betaParam=beta, **kw)
     return it, time.perf_counter() - t
 
 

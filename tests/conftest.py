@@ -167,6 +167,37 @@ def stamp_case(j, i, variant=LIBM):
     return z[f"cut{j}"], psf, np.float64(z[f"bkg{j}"]), kw, ref
 
 
+def stamp_kl_case(j, variant=LIBM):
+    """Inputs and reference outputs of one KL star-stamp run (make_golden.py
+    stamps_kl; application_sgp_star_stamps.py:107-112, the USE_BETADIV=False
+    branch): the 31x31 float32 cutout, the >f8 DIAPL PSF, the float64 median
+    background, the kwargs with the star's flux, and the reference's x / iters /
+    discr / line-search trials per iteration (fixture set `variant`)."""
+    key = "kl" + variant
+    if key not in _STAMPS:
+        _STAMPS[key] = golden(f"ref_stamps31_kl{variant}.npz")
+    z = _STAMPS[key]
+    import fits_io
+    _, psf = fits_io.read_fits(os.path.join(GOLDEN, "psfccfbrd210048_1_1_img.fits"))
+    kw = ref_kwargs(z)
+    kw.update(flux=np.float64(z[f"flux{j}"]))
+    ref = {k: z[f"{k}{j}"] for k in ("x", "iters", "discr", "trials")}
+    return z[f"cut{j}"], psf, np.float64(z[f"bkg{j}"]), kw, ref
+
+
+def stamp_kl_exact(x, it, discr, trials, ref, xtol=1e-5, drtol=1e-7):
+    """The KL stamp bar: the reference's iteration count and its line-search
+    trial count in every iteration, x within the north-star 1e-5, the
+    discrepancy at rtol 1e-7 (no float32 power enters the KL objective)."""
+    assert it == int(ref["iters"]), (it, int(ref["iters"]))
+    np.testing.assert_array_equal(np.asarray(trials, dtype=np.int64),
+                                  np.asarray(ref["trials"], dtype=np.int64))
+    r = float(np.linalg.norm(x - ref["x"]) / np.linalg.norm(ref["x"]))
+    assert r < xtol, r
+    np.testing.assert_allclose(discr, ref["discr"], rtol=drtol)
+    return r
+
+
 def konst_ulp_discr(gn, beta, n_ulp=4):
     """Discrepancy change of n_ulp float32 ulps of K = sum(s*gn**beta) on a
     float32 image: numpy's float32 power is not correctly rounded (SVML), the

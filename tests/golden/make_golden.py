@@ -8,7 +8,7 @@ outputs); this script is how they were made:
     cd /root/repo && PYTHONDONTWRITEBYTECODE=1 /opt/conda/bin/python3.9 tests/golden/make_golden.py linear
     cd /root/repo && PYTHONDONTWRITEBYTECODE=1 /opt/conda/bin/python3.9 tests/golden/make_golden.py app
     cd /root/repo && NPY_DISABLE_CPU_FEATURES="$LIBM_FEATURES" PYTHONDONTWRITEBYTECODE=1 \
-        /opt/conda/bin/python3.9 tests/golden/make_golden.py stamps   # (and app)
+        /opt/conda/bin/python3.9 tests/golden/make_golden.py stamps   # (and app, stamps_kl)
 
   with LIBM_FEATURES="AVX2 FMA3 AVX512F AVX512CD AVX512_KNL AVX512_KNM AVX512_SKX AVX512_CLX
   AVX512_CNL AVX512_ICL": numpy 1.26 then evaluates float32 ``**`` and ``log``
@@ -138,6 +138,23 @@ def run_quiet(fn, *a, **k):
         return fn(*a, **k)
 
 
+class _CountingNumpy(types.ModuleType):
+    """numpy for the reference's sgp module, with np.log counted (each KL
+    line-search trial evaluates np.log once, restoration/sgp.py:334; the setup
+    once, :265)."""
+
+    def __init__(self, seq):
+        super().__init__("numpy")
+        self._seq = seq
+
+    def __getattr__(self, k):
+        return getattr(np, k)
+
+    def log(self, *a, **k):
+        self._seq.append("b")
+        return np.log(*a, **k)
+
+
 def run_counted(sgp, fn, *a, stdout=None, **k):
     """run_quiet(getattr(sgp, fn), ...) that also returns the reference's
     line-search trials of every iteration: the calls of the module-level
@@ -158,6 +175,9 @@ def run_counted(sgp, fn, *a, stdout=None, **k):
         return op(*x, **y)
 
     sgp.betaDiv, sgp.projectDF = b, p
+    onp = sgp.np
+    if fn == "sgp":  # the KL loop evaluates its objective inline: count its np.log calls
+        sgp.np = _CountingNumpy(seq)
     try:
         import contextlib
         import io
@@ -165,6 +185,7 @@ def run_counted(sgp, fn, *a, stdout=None, **k):
             out = getattr(sgp, fn)(*a, **k)
     finally:
         sgp.betaDiv, sgp.projectDF = ob, op
+        sgp.np = onp
     trials, cur = [], None
     for s in seq:
         if s == "p":
@@ -523,6 +544,40 @@ def make_stamps():
     np.savez_compressed(os.path.join(OUT, f"ref_stamps31{_suffix()}.npz"), **out)
 
 
+def make_stamps_kl():
+    """The KL branch of the star-stamp application
+    (application_sgp_star_stamps.py:107-112, USE_BETADIV False): sgp(...) on
+    the same 8 float32 31x31 cutouts as make_stamps, with the default circular
+    A, DEFAULT_PARAMS (alpha 10), proj_type 1, init_recon 2, stop rule 3
+    (tol_convergence default 1e-4), MAXIT 500, flux and the median background
+    as there.  Records x, iters, discr and the line-search trials of every
+    iteration (np.log calls of the KL loop, run_counted)."""
+    sgp, fcp = import_reference(need_astropy=True)
+    from astropy.io import fits
+    from astropy.nddata import Cutout2D
+    img = fits.getdata("/root/reference/results/SUBDIV_ORIGIMG.fits")  # (375, 375) >f4
+    psf = fits.getdata("/root/reference/psf/psfccfbrd210048_1_1_img.fits")  # (31, 31) >f8
+    pos = star_positions(img, 8)
+    max_projs, gamma, beta, alpha_min, alpha_max, alpha, M_alpha, tau, M = sgp.DEFAULT_PARAMS
+    kw = dict(gamma=gamma, beta=beta, alpha_min=alpha_min, alpha_max=alpha_max, alpha=alpha,
+              M_alpha=M_alpha, tau=tau, M=M, proj_type=1, max_projs=max_projs, init_recon=2,
+              stop_criterion=3, save=False, verbose=True, ccd_sat_level=65000, scale_data=True)
+    out = {"pos": np.array(pos, dtype=np.int32)}
+    for j, (x, y) in enumerate(pos):
+        cut = Cutout2D(img, (x, y), size=31).data
+        assert cut.shape == (31, 31) and cut.dtype == np.dtype(">f4")
+        bkg = np.float64(np.median(cut))
+        flux = np.float64(np.sum(cut - bkg))
+        out[f"bkg{j}"], out[f"flux{j}"], out[f"cut{j}"] = bkg, flux, cut
+        (x_, it, discr, _, _), trials = run_counted(sgp, "sgp", cut, psf, bkg, flux=flux, **kw)
+        assert len(trials) == it
+        out[f"x{j}"], out[f"iters{j}"], out[f"discr{j}"], out[f"trials{j}"] = x_, it, discr, trials
+        print(f"KL stamp {j} at {x, y}: iters {it}, trials {trials.tolist()}")
+    out["kwargs"] = repr(kw)
+    out["numpy_cpu_features"] = os.environ.get("NPY_DISABLE_CPU_FEATURES", "")
+    np.savez_compressed(os.path.join(OUT, f"ref_stamps31_kl{_suffix()}.npz"), **out)
+
+
 def make_c4():
     """BASELINE config C4's field (2048x2048, 5000 stars, 64x64
     Gaussian PSF embedded at the centre, circular A, beta = 1.05, projection)
@@ -735,6 +790,36 @@ def make_satellite():
               f"[{min(ens):.6f}, {max(ens):.6f}], x rel up to {max(ens_x):.2e}")
 
 
+def make_satellite_ensemble_discr():
+    """The satellite runs' one-ulp ensemble (make_satellite) again, recording
+    the discrepancy trajectory of every member: for each iteration the largest
+    relative deviation of a member's discrepancy from the reference's own run.
+    Where that stays <= 1e-7 the trajectory is not yet chaotic at the test's
+    tolerance, so a faithful restatement must follow the reference there."""
+    from scipy.io import loadmat
+    sgp, fcp = import_reference(need_astropy=False)
+    sat = loadmat(os.path.join(REF, "simulated_test/data/satellite_25500.mat"))
+    image, psf, bkg = sat["gn"], sat["psf"], sat["bg"][0][0]
+    runs = {"sat_kl332": ("sgp", dict(init_recon=3, stop_criterion=1, MAXIT=332)),
+            "sat_beta332": ("sgp_betaDiv", dict(init_recon=3, stop_criterion=1, MAXIT=332,
+                                                betaParam=1.0001, lr=1e-3, lr_exp_param=0.1,
+                                                schedule_lr=True, adapt_beta=False))}
+    for name, (fn, kw) in runs.items():
+        _, _, discr, _, _ = run_quiet(getattr(sgp, fn), image, psf, bkg, **kw)
+        dev = np.zeros_like(discr)
+        for seed in range(8):
+            sg = np.random.default_rng(seed).choice([-1.0, 1.0], image.shape)
+            gp = image * (1.0 + sg * 2.0 ** -52)
+            _, _, de, _, _ = run_quiet(getattr(sgp, fn), gp, psf, bkg, **kw)
+            dev = np.maximum(dev, np.abs(de / discr - 1))
+        k = int(np.argmax(dev > 1e-7)) - 1 if np.any(dev > 1e-7) else len(dev) - 1
+        np.savez_compressed(os.path.join(OUT, f"ref_{name}_ensdiscr.npz"), discr=discr,
+                            discr_dev=dev, last_1e7=k)
+        print(f"{name}: ensemble discrepancy within 1e-7 of the reference through iteration {k}; "
+              f"deviation at 50/100/200/332: {dev[50]:.1e} {dev[100]:.1e} {dev[200]:.1e} "
+              f"{dev[-1]:.1e}")
+
+
 def make_crowded():
     """The application's CROWDED mode (application_sgp_subdivisions.py:22,
     44-50, 84-115): the whole 450x450 float32 frame
@@ -797,6 +882,10 @@ if __name__ == "__main__":
                 make_long()
             elif which == "long_ens":
                 make_long_ensemble()
+            elif which == "satellite_ens":
+                make_satellite_ensemble_discr()
+            elif which == "stamps_kl":
+                make_stamps_kl()
             elif which == "c4":
                 make_c4()
             elif which == "stamps":

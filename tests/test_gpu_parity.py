@@ -200,13 +200,30 @@ def test_satellite_332_known_answer(sgpmod, name):
     rel_err in [0.2900, 0.2956] (KL) / [0.2898, 0.2971] (beta) and moves x by
     up to 7.7e-2 / 6.8e-2.  The device's FFT and sums round differently, so
     its rel_err and x must lie within 1.5x that ensemble's largest deviation
-    from the reference's run; its discrepancy follows the reference's through
-    iteration 50 (before the chaos: 1.8e-11 in that ensemble) at 1e-7."""
-    from conftest import satellite_case
+    from the reference's run.
+
+    How this bar came about: the first bar tried (round 4) was 3x the spread
+    the reference itself shows with scipy.fft in place of numpy's FFT (2.1e-4
+    KL / 3.2e-4 beta in rel_err); the device missed it (|d rel_err| 9.1e-4
+    KL, 1.40e-3 beta; gpurun_out/r04b_tests.log), because one FFT swap is a
+    single sample of the chaos, not its width.  The 1-ulp ensemble measures
+    that width; by itself it pins little beyond "the same attractor".
+
+    The non-chaotic part is pinned tightly (make_golden.py satellite_ens):
+    the ensemble's discrepancies stay within 1e-7 of the reference's run
+    through iteration 94 (KL) / 102 (beta), so the device's must follow the
+    reference's there at rtol 1e-7 too."""
+    from conftest import golden, satellite_case
     gn, psf, bkg, obj, kw, fn, fx = satellite_case(name)
     x, it, discr, _, _ = getattr(sgpmod, fn)(gn, psf, bkg, **kw)
     assert it == 332 and len(discr) == 333
-    np.testing.assert_allclose(discr[:51], fx["discr"][:51], rtol=1e-7)
+    ens = golden(f"ref_{name}_ensdiscr.npz")
+    k = int(ens["last_1e7"])
+    assert k >= 90, k
+    dev = np.abs(discr / fx["discr"] - 1)
+    print(name, "device discrepancy deviation at 50/94/100/200/332:", dev[[50, 94, 100, 200, 332]],
+          "ensemble:", ens["discr_dev"][[50, 94, 100, 200, 332]])
+    np.testing.assert_allclose(discr[:k + 1], fx["discr"][:k + 1], rtol=1e-7)
     relerr = float(np.sqrt(np.sum((x - obj) ** 2) / np.sum(obj * obj)))
     ref = float(fx["relerr"])
     spread = float(np.max(np.abs(fx["relerr_ulp_ensemble"] - ref)))

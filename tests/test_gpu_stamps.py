@@ -143,3 +143,40 @@ def test_star_stamps_float32_storage(sgpmod, team):
         r = np.linalg.norm(f["x"][0] - a["x"][0]) / np.linalg.norm(a["x"][0])
         assert r < 1e-3, (j, i, r)
         np.testing.assert_allclose(f["discr"][0], a["discr"][0], rtol=1e-3)
+
+
+def test_star_stamps_kl_branch(sgpmod, monkeypatch):
+    """The KL branch of the star-stamp application (USE_BETADIV False,
+    application_sgp_star_stamps.py:107-112): sgp(...) on the 8 float32
+    cutouts, default circular A, stop rule 3, against the reference's runs
+    (make_golden.py stamps_kl) in both fixture sets: its iteration count and
+    line-search trial count in every iteration, x within 1e-5, discrepancy at
+    rtol 1e-7.  The 8 runs as one batched launch; each also through the
+    single-image drop-in, alone (automatic team: the same bar without the trial
+    counts, which the drop-in does not return) and at team 1 (bitwise the
+    batch)."""
+    from conftest import LIBM, stamp_kl_case, stamp_kl_exact
+    cases = [stamp_kl_case(j) for j in range(8)]
+    gns = np.stack([c[0] for c in cases])
+    psf = cases[0][1]
+    bkgs = np.array([c[2] for c in cases])
+    flux = np.array([c[3]["flux"] for c in cases])
+    kw = {k: v for k, v in cases[0][3].items() if k != "flux"}
+    out = sgpmod.sgp_batch(gns, psf, bkgs, flux=flux, team=1, **kw)
+    worst = 0.0
+    for j, (gn, p, b, k, ref) in enumerate(cases):
+        it = int(out["iters"][j])
+        for variant in (LIBM, SVML):
+            r = stamp_kl_exact(out["x"][j], it, out["discr"][j, :it + 1], trials_of(out, j, it),
+                               stamp_kl_case(j, variant)[4])
+            worst = max(worst, r)
+        x2, it2, d2, _, _ = sgpmod.sgp(gn, p, b, **k)  # automatic team
+        stamp_kl_exact(x2, it2, d2, ref["trials"], ref)
+    monkeypatch.setattr(sgpmod, "TEAM_DEFAULT", 1)
+    for j in (0, 5):
+        gn, p, b, k, _ = cases[j]
+        x1, it1, d1, _, _ = sgpmod.sgp(gn, p, b, **k)
+        assert it1 == int(out["iters"][j])
+        np.testing.assert_array_equal(x1, out["x"][j])
+        np.testing.assert_array_equal(d1, out["discr"][j, :it1 + 1])
+    print("KL stamps: x rel to the reference at most", worst)

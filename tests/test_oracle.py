@@ -139,6 +139,21 @@ def test_oracle_star_stamps_adaptive_float32():
     assert parted[(0, 4)][0] == 33
 
 
+@pytest.mark.parametrize("variant", ["_libm", ""])
+def test_oracle_star_stamps_kl_float32(variant):
+    """The KL branch of the star-stamp application (make_golden.py stamps_kl,
+    application_sgp_star_stamps.py:107-112): the oracle takes the reference's
+    iteration and trial counts in every iteration of all 8 runs, x within
+    1e-5 and the discrepancy at rtol 1e-7, against both fixture sets."""
+    import sgp_oracle as orc
+    from conftest import stamp_kl_case, stamp_kl_exact
+    for j in range(8):
+        gn, psf, bkg, kw, ref = stamp_kl_case(j, variant)
+        st = {}
+        x, it, discr, _, _ = orc.sgp(gn, psf, bkg, stats=st, **kw)
+        stamp_kl_exact(x, it, discr, st["ls_trials"], ref)
+
+
 # ------------------------------------------------- application drop-in path
 from conftest import APP_CASES, app_case  # noqa: E402
 

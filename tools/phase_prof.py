@@ -14,6 +14,8 @@ import ctypes
 import os
 import sys
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "beta-sgp_amd")):
     sys.path.insert(0, p)
@@ -48,9 +50,19 @@ def main():
     L = _bsgp.lib()
     L.bsgp_phase_prof.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
     buf = (ctypes.c_uint64 * 32)()
-    cfg = bench.CONFIGS[args.config]
-    B = args.batch or cfg["batch"]
-    if cfg.get("stamps"):  # the star-stamp workload (bench.py stamps31), phase kernels
+    if args.config == "app375":  # one application subdivision (bench.py app375), automatic team
+        img, psf, bk, akw, betas = bench.app375_inputs()
+        gn = torch.from_numpy(np.asarray(img, dtype=np.float32).copy()).cuda()[None]
+        bkg = torch.from_numpy(np.asarray(bk, dtype=np.float64)).cuda()[None]
+        kw = {k: v for k, v in akw.items() if k not in ("save", "verbose", "flux")}
+        kw.update(betaParams=[betas[0]], flux=np.array([akw["flux"]]), streams=args.streams)
+        cfg, B = {}, 1
+    else:
+        cfg = bench.CONFIGS[args.config]
+        B = args.batch or cfg["batch"]
+    if args.config == "app375":
+        pass
+    elif cfg.get("stamps"):  # the star-stamp workload (bench.py stamps31), phase kernels
         cuts, psf, bk, fl, betas = bench.stamp_inputs(B)
         gn = cuts
         bkg = bk
