@@ -371,6 +371,9 @@ int bsgp_plan_create_checked(int32_t H, int32_t W, const double* psf, int32_t kh
     g.Q = next_fast_len(qmin);
   }
   g.Qh = g.Q / 2 + 1;
+  // stored half spectrum: column k at k * sld (BSGP_SPEC_PAD rows of padding
+  // break a power-of-two column stride; even, so row pairs stay 32-B aligned)
+  g.sld = H + ((H & 1) ? 1 : 0) + BSGP_SPEC_PAD;
   g.fp.n = g.P;
   g.fq.n = g.Q;
   if (!plan_radices(g.P, g.fp.radix, &g.fp.ns) || !plan_radices(g.Q, g.fq.radix, &g.fq.ns)) {
@@ -572,10 +575,10 @@ int bsgp_plan_create_checked(int32_t H, int32_t W, const double* psf, int32_t kh
   p->storage = storage;
   // slot: gn and bkg in float64 (vec_stride each), the seven iteration vectors
   // in the storage type, then the half spectrum (complex float64)
-  p->vec_stride = round_up(N, 32);
+  p->vec_stride = round_up(N, 32) + BSGP_VEC_PAD;
   const size_t vbytes = storage == BSGP_STORAGE_F32 ? sizeof(float) : sizeof(double);
   p->spec_off = 2 * p->vec_stride + 7 * p->vec_stride * vbytes / sizeof(double);
-  p->slot_stride = p->spec_off + round_up((size_t)H * g.Qh * 2, 32);
+  p->slot_stride = p->spec_off + round_up((size_t)g.sld * g.Qh * 2, 32);
   {
     const std::vector<int> prog = pairwise_program((long)N, &p->pw);
     if (hipMalloc(&p->pwprog, prog.size() * sizeof(int)) != hipSuccess ||
@@ -1046,7 +1049,7 @@ int bsgp_apply_operator(bsgp_plan p, int32_t B, int32_t transpose, const double*
   // spectrum per image; many images: one persistent workgroup per image
   const bool split = (size_t)B * 4 <= (size_t)slots;
   const int grid = split ? B : (B < slots ? B : slots);
-  const size_t stride = round_up((size_t)p->g.H * p->g.Qh, 16);
+  const size_t stride = round_up((size_t)p->g.sld * p->g.Qh, 16);
   if ((size_t)grid > p->opws_slots) {
     if (p->opws) HIP_TRY(hipFree(p->opws));
     p->opws = nullptr;

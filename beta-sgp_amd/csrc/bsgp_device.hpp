@@ -67,6 +67,7 @@ struct Geo {
                  // workgroups per CU; == nfw otherwise)
   int coop;      // 1: thread groups of the workgroup run the transforms (long rows/columns)
   int lpad;      // complex elements per LDS buffer (odd: spreads banks)
+  int sld;       // column stride of the stored half spectrum (>= H, even; BSGP_SPEC_PAD)
   FftPlan fp;    // length P (columns)
   FftPlan fq;    // length Q (rows)
   const cd* tfA;   // [Qh][P] transfer function of A, scaled by 1/(P*Q)
@@ -657,7 +658,7 @@ __device__ __forceinline__ void coop_gather_1(const Geo& G, const cd* spec, int 
 #pragma unroll
     for (int u = 0; u < kCCH; ++u) {  // clamped, branch-free
       const int k = min(k0 + t + kBlock * u, G.Qh - 1);
-      const cd* col = spec + (size_t)k * G.H + r;
+      const cd* col = spec + (size_t)k * G.sld + r;
       A[u] = col[0];
       const cd b = col[two ? 1 : 0];
       B[u] = two ? b : cmk(0.0, 0.0);
@@ -711,7 +712,7 @@ template <class CP>
 __device__ __forceinline__ void coop_row_inv_fwd_1(const Geo& G, const Part& D, cd* spec, cd* lds,
                                                  CP& cp) {
   const int t = threadIdx.x;
-  const bool pair_ok = (G.H & 1) == 0;
+  const bool pair_ok = (G.sld & 1) == 0;
   cd* a = lds;
   cd* b = lds + G.lpad;
   for (int r = 2 * D.gw0; r < G.H; r += 2 * D.gws) {
@@ -733,7 +734,7 @@ __device__ __forceinline__ void coop_row_inv_fwd_1(const Geo& G, const Part& D, 
     for (int k = t; k < G.Qh; k += kBlock) {
       cd ak, bk;
       r2c_split(Y, G.Q, k, &ak, &bk);
-      store_pair(spec + (size_t)k * G.H + r, two, pair_ok, ak, bk);
+      store_pair(spec + (size_t)k * G.sld + r, two, pair_ok, ak, bk);
     }
     __syncthreads();
   }
@@ -754,7 +755,7 @@ __device__ __forceinline__ void coop_col_pair_nyq(const Geo& G, cd* spec, const 
                                                   cd* b) {
   const int t = threadIdx.x;
   cd* c0 = spec;
-  cd* cN = spec + (size_t)(G.Qh - 1) * G.H;
+  cd* cN = spec + (size_t)(G.Qh - 1) * G.sld;
   const cd* t0 = tf;
   const cd* tN = tf + (size_t)(G.Qh - 1) * G.P;
   for (int p0 = 0; p0 < G.P; p0 += kBlock * kCCH) {
@@ -801,7 +802,7 @@ __device__ __forceinline__ void coop_col_conv_1(const Geo& G, const Part& D, cd*
       coop_col_pair_nyq(G, spec, tf, a, b);
       continue;
     }
-    cd* col = spec + (size_t)k * G.H;
+    cd* col = spec + (size_t)k * G.sld;
     const cd* tk = tf + (size_t)k * G.P;
     for (int p0 = 0; p0 < G.P; p0 += kBlock * kCCH) {
       cd cv[kCCH];
@@ -910,7 +911,7 @@ __device__ __forceinline__ void coop_gather_g(const Geo& G, const cd* spec, int 
 #pragma unroll
     for (int u = 0; u < kCCH; ++u) {  // clamped, branch-free
       const int k = min(k0 + t + c.nt * u, G.Qh - 1);
-      const cd* col = spec + (size_t)k * G.H + r;
+      const cd* col = spec + (size_t)k * G.sld + r;
       A[u] = col[0];
       const cd b = col[two ? 1 : 0];
       B[u] = two ? b : cmk(0.0, 0.0);
@@ -976,7 +977,7 @@ __device__ __forceinline__ void coop_row_inv_fwd_g(const Geo& G, const Part& D, 
                                                    CP& cp) {
   const CGrp c = coop_grp(D.nf);
   const int t = c.t;
-  const bool pair_ok = (G.H & 1) == 0;
+  const bool pair_ok = (G.sld & 1) == 0;
   cd* a = lds + c.g * 2 * G.lpad;
   cd* b = a + G.lpad;
   for (int r0 = 2 * D.gw0; r0 < G.H; r0 += 2 * D.gws) {
@@ -1009,7 +1010,7 @@ __device__ __forceinline__ void coop_row_inv_fwd_g(const Geo& G, const Part& D, 
       for (int k = t; k < G.Qh; k += c.nt) {
         cd ak, bk;
         r2c_split(Y, G.Q, k, &ak, &bk);
-        store_pair(spec + (size_t)k * G.H + r, two, pair_ok, ak, bk);
+        store_pair(spec + (size_t)k * G.sld + r, two, pair_ok, ak, bk);
       }
     }
     __syncthreads();
@@ -1026,7 +1027,7 @@ __device__ __forceinline__ void coop_col_conv_g(const Geo& G, const Part& D, cd*
   for (int k0 = D.gw0; k0 < G.Qh; k0 += D.gws) {
     const int k = k0 + c.g;
     const bool act = k < G.Qh;
-    cd* col = spec + (size_t)k * G.H;
+    cd* col = spec + (size_t)k * G.sld;
     const cd* tk = tf + (size_t)k * G.P;
     PH_T(tq0);
     if (act) {
@@ -1154,16 +1155,19 @@ __device__ __forceinline__ void row_fwd2(const Geo& G, const Part& D, int nrows,
         // (loads past the row end are clamped, not skipped: a skipped load
         // would be a branch whose join waits for every load in flight)
         for (int j0 = 0; j0 < G.Q; j0 += 2 * S) {
-          load_rows<JCH>(ld, r, two, j0 + S, lane, ncols, u0, u1);
+          // (no loads for batches wholly in the zero padding, j >= ncols)
+          if (j0 + S < ncols) load_rows<JCH>(ld, r, two, j0 + S, lane, ncols, u0, u1);
           put(j0, v0, v1);
           if (j0 + S < G.Q) {
-            load_rows<JCH>(ld, r, two, j0 + 2 * S, lane, ncols, v0, v1);
+            if (j0 + 2 * S < ncols) load_rows<JCH>(ld, r, two, j0 + 2 * S, lane, ncols, v0, v1);
             put(j0 + S, u0, u1);
           }
         }
       } else {
         for (int j0 = 0; j0 < G.Q; j0 += 64 * JCH) {
-          if (!PF || j0 > 0) load_rows<JCH>(ld, r, two, j0, lane, ncols, v0, v1);
+          // batches wholly in the zero padding (j0 >= ncols: the 256..269 of a
+          // 270-point row) load nothing: put() writes zeros there
+          if ((!PF || j0 > 0) && j0 < ncols) load_rows<JCH>(ld, r, two, j0, lane, ncols, v0, v1);
           put(j0, v0, v1);
         }
       }
@@ -1269,7 +1273,7 @@ __device__ __forceinline__ void row_inv2(const Geo& G, const Part& D, const cd* 
     cd* other = in + G.lpad;
     int r = 2 * (D.gw0 + w);
     PH_SUB_T(tph);
-    if (r < G.H) gather_pair(G, spec, G.H, r, (r + 1) < G.H, in, lane);
+    if (r < G.H) gather_pair(G, spec, G.sld, r, (r + 1) < G.H, in, lane);
     for (; r < G.H; r += 2 * D.gws) {
       const bool two = (r + 1) < G.H;
       V v0[JCH], v1[JCH];
@@ -1281,7 +1285,7 @@ __device__ __forceinline__ void row_inv2(const Geo& G, const Part& D, const cd* 
       cd* F = (Z == in) ? other : in;
       const int rn = r + 2 * D.gws;
       const bool next = rn < G.H, two_n = (rn + 1) < G.H;
-      if (next) stage_pair(G, spec, G.H, rn, two_n, F, lane);
+      if (next) stage_pair(G, spec, G.sld, rn, two_n, F, lane);
       auto eat = [&](int j0, const V (&w0)[JCH], const V (&w1)[JCH]) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < JCH; ++u) {
@@ -1345,13 +1349,13 @@ __device__ __forceinline__ void row_inv_fwd(const Geo& G, const Part& D, cd* spe
     return;
   }
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bool pair_ok = (G.H & 1) == 0;
+  const bool pair_ok = (G.sld & 1) == 0;
   if (w < G.nfw) {
     cd* a = lds + w * 2 * G.lpad;
     cd* b = a + G.lpad;
     for (int r = 2 * (D.gw0 + w); r < G.H; r += 2 * D.gws) {
       const bool two = (r + 1) < G.H;
-      gather_pair(G, spec, G.H, r, two, a, lane);
+      gather_pair(G, spec, G.sld, r, two, a, lane);
       wave_sync();
       cd* Z = fft_any(a, b, G.fq, true, lane, 64, WaveSync());
       cd* in2 = (Z == a) ? b : a;
@@ -1369,7 +1373,7 @@ __device__ __forceinline__ void row_inv_fwd(const Geo& G, const Part& D, cd* spe
       for (int k = lane; k < G.Qh; k += 64) {
         cd ak, bk;
         r2c_split(Y, G.Q, k, &ak, &bk);
-        store_pair(spec + (size_t)k * G.H + r, two, pair_ok, ak, bk);
+        store_pair(spec + (size_t)k * G.sld + r, two, pair_ok, ak, bk);
       }
       wave_sync();
     }
@@ -1400,7 +1404,7 @@ __device__ __forceinline__ void col_conv(const Geo& G, const Part& D, cd* spec, 
     // in registers across it), or the TF loaded after the FFT
     const bool one = BSGP_COL_TFPRE && G.P <= 64 * kPCH;
     for (int k = D.gw0 + w; k < G.Qh; k += D.gws) {
-      cd* col = spec + (size_t)k * G.H;
+      cd* col = spec + (size_t)k * G.sld;
       const cd* t = tf + (size_t)k * G.P;
       cd tv[kPCH];
       for (int p0 = 0; p0 < G.P; p0 += 64 * kPCH) {

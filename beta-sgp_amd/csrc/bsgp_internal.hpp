@@ -157,6 +157,12 @@ void persist_kernels_all(std::vector<const void*>& f);
 #ifndef BSGP_COOP_GROUPS
 #define BSGP_COOP_GROUPS 4
 #endif
+#ifndef BSGP_SPEC_PAD
+#define BSGP_SPEC_PAD 0  // rows of padding per stored spectrum column (even)
+#endif
+#ifndef BSGP_VEC_PAD
+#define BSGP_VEC_PAD 0  // elements of padding after every per-image slot vector (multiple of 32)
+#endif
 #ifndef BSGP_COOP_ELEMS
 #define BSGP_COOP_ELEMS 8  // elements per thread a group may take when one batch leaves one group
 #endif

@@ -545,7 +545,7 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
         reinterpret_cast<float*>(B.dtf), D, tm);
   }
   double fsum[3] = {0.0, 0.0, 0.0};  // K, T0, T1
-  row_fwd<COOP>(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.xa[r * G.W + j]; });
+  row_fwd<COOP>(G, D, G.H, G.W, G.sld, B.spec, lds, [&](int r, int j) { return B.xa[r * G.W + j]; });
   team_sync(tm);
   col_conv<COOP>(G, D, B.spec, tf_of(G, img, 0), lds);
   team_sync(tm);
@@ -574,7 +574,7 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   });
   team_sync(tm);  // every row of spec read before it is overwritten
   // scaling-matrix bounds from AT(gn) (sgp.py:268-273)
-  row_fwd<COOP>(G, D, G.H, G.W, G.H, B.spec, lds, [&](int r, int j) { return B.gns[r * G.W + j]; });
+  row_fwd<COOP>(G, D, G.H, G.W, G.sld, B.spec, lds, [&](int r, int j) { return B.gns[r * G.W + j]; });
   team_sync(tm);
   col_conv<COOP>(G, D, B.spec, tf_of(G, img, 1), lds);
   team_sync(tm);
@@ -936,7 +936,7 @@ __device__ __forceinline__ void dir_phase(const SolveArgs& A, int img) {
   PH_T(tk1);
   double gd[1] = {0.0};
   row_fwd2<BSGP_DIR_JCH, BSGP_DIR_PF, BSGP_DIR_COMP, COOP, false, 22>(
-      G, Pt, G.H, G.W, G.H, B.spec, lds,
+      G, Pt, G.H, G.W, G.sld, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
         return double2{B.xa[i], B.ga[i]};
@@ -1333,7 +1333,7 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
     double x, d, g, bkv, p0;
   };
   row_fwd2<BSGP_LSACC_JCH, BSGP_LSACC_PF, BSGP_LS_COMP, COOP, BSGP_LSACC_PIPE, 16>(
-      G, Pt, G.H, G.W, G.H, B.spec, lds,
+      G, Pt, G.H, G.W, G.sld, B.spec, lds,
       [&](int r, int j) {
         const int i = r * G.W + j;
         AcIn q;

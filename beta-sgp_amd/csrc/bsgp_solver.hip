@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(kBlock) apply_op_kernel(Geo G, int B, int tran
     const double* xi = x + (size_t)img * N;
     double* oi = out + (size_t)img * N;
     const Part D = solo_part(G.nfw);
-    row_fwd<COOP>(G, D, G.H, G.W, G.H, spec, lds, [&](int r, int j) { return xi[r * G.W + j]; });
+    row_fwd<COOP>(G, D, G.H, G.W, G.sld, spec, lds, [&](int r, int j) { return xi[r * G.W + j]; });
     __syncthreads();
     col_conv<COOP>(G, D, spec, tf_of(G, img, transpose), lds);
     row_inv<COOP>(G, D, spec, lds, [&](int r, int j, double v) { oi[r * G.W + j] = v; });
@@ -190,7 +190,7 @@ __global__ void __launch_bounds__(kBlock) op_rows_kernel(Geo G, const double* x,
   D.gw0 = blockIdx.x * G.nfw;
   D.gws = gridDim.x * G.nfw;
   load_tw_lds(G);
-  row_fwd<COOP>(G, D, G.H, G.W, G.H, specws + blockIdx.y * spec_stride, lds,
+  row_fwd<COOP>(G, D, G.H, G.W, G.sld, specws + blockIdx.y * spec_stride, lds,
                 [&](int r, int j) { return xi[r * G.W + j]; });
 }
 template <bool COOP>

@@ -369,7 +369,7 @@ def test_no_positive_scaling_bound_raises_like_reference(sgpmod, persistent):
         np.testing.assert_array_equal(out["x"][i].cpu().numpy(), one["x"][0])
 
 
-def test_float32_psf_accepted_by_batch_like_dropin(sgpmod):
+def test_float32_psf_accepted_by_batch_like_dropin(sgpmod, monkeypatch):
     """A float32 PSF normalised in float32 (float32 sum exactly 1, float64 sum
     off by more than 1e4*eps) passes the reference's check (sgp.py:97-102 sums
     in the PSF's dtype): the single-image drop-in and the batch API accept it
@@ -381,6 +381,7 @@ def test_float32_psf_accepted_by_batch_like_dropin(sgpmod):
     kw.update(MAXIT=8)
     gn = fx["gn"].astype(np.float64)
     p = _f32_psf_sum_exact(1)
+    monkeypatch.setattr(sgpmod, "TEAM_DEFAULT", 1)  # the batch's team size: the same bits
     x, it, _, _, _ = sgpmod.sgp_betaDiv(gn, p, np.float64(100.0), **kw)
     b = kw.pop("betaParam")
     out = sgpmod.sgp_betaDiv_batch(gn[None], p, 100.0, betaParams=[b], team=1, **kw)

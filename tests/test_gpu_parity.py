@@ -209,10 +209,14 @@ def test_satellite_332_known_answer(sgpmod, name):
     single sample of the chaos, not its width.  The 1-ulp ensemble measures
     that width; by itself it pins little beyond "the same attractor".
 
-    The non-chaotic part is pinned tightly (make_golden.py satellite_ens):
-    the ensemble's discrepancies stay within 1e-7 of the reference's run
-    through iteration 94 (KL) / 102 (beta), so the device's must follow the
-    reference's there at rtol 1e-7 too."""
+    The non-chaotic part is pinned iteration by iteration (make_golden.py
+    satellite_ens): the ensemble's discrepancies stay within 1e-7 of the
+    reference's run through iteration 94 (KL) / 102 (beta); there the
+    device's relative deviation from the reference's discrepancy must stay
+    within 3x the ensemble's at the same iteration (floor 1e-10).  Measured:
+    the device runs at ~1.4x the ensemble (KL: 6.2e-11 vs 4.4e-11 at
+    iteration 50, 8.1e-8 vs 5.7e-8 at 94) -- its FFT and sums round
+    differently at every step, not only once at the input."""
     from conftest import golden, satellite_case
     gn, psf, bkg, obj, kw, fn, fx = satellite_case(name)
     x, it, discr, _, _ = getattr(sgpmod, fn)(gn, psf, bkg, **kw)
@@ -223,7 +227,9 @@ def test_satellite_332_known_answer(sgpmod, name):
     dev = np.abs(discr / fx["discr"] - 1)
     print(name, "device discrepancy deviation at 50/94/100/200/332:", dev[[50, 94, 100, 200, 332]],
           "ensemble:", ens["discr_dev"][[50, 94, 100, 200, 332]])
-    np.testing.assert_allclose(discr[:k + 1], fx["discr"][:k + 1], rtol=1e-7)
+    bar = np.maximum(3.0 * ens["discr_dev"][:k + 1], 1e-10)
+    over = np.nonzero(dev[:k + 1] > bar)[0]
+    assert over.size == 0, (name, over[:5], dev[over[:5]], bar[over[:5]])
     relerr = float(np.sqrt(np.sum((x - obj) ** 2) / np.sum(obj * obj)))
     ref = float(fx["relerr"])
     spread = float(np.max(np.abs(fx["relerr_ulp_ensemble"] - ref)))
