@@ -174,6 +174,11 @@ struct bsgp_plan_s {
   size_t st_n = 0;
   int* active = nullptr;     // device counter of images still iterating
   int* active_h = nullptr;   // pinned host mirror for polling
+  int* done_h = nullptr;     // host-mapped: the solve seq once every image has stopped
+  int* done_d = nullptr;     // (its device address)
+  int seq = 0;               // solves started on this plan
+  static constexpr int kPollRing = 8;
+  hipEvent_t ev_it[kPollRing] = {};  // after iteration it on stream 0 (lookahead polling)
   // sub-batch streams: phases of different sub-batches overlap on the device
   static constexpr int kMaxStreams = 16;
   hipStream_t sub[kMaxStreams] = {};
@@ -461,6 +466,29 @@ int bsgp_plan_create_checked(int32_t H, int32_t W, const double* psf, int32_t kh
   // budget (one table when P == Q), else they read the global table (as the
   // cooperative workgroup-wide transforms always do)
   g.fp.lds_tw = g.fq.lds_tw = -1;
+  g.fp.lds_tw2 = g.fq.lds_tw2 = -1;
+  g.tw2 = 0;
+  // cooperative 2048-point transforms (fft_wide's static plan): their twiddles
+  // as a two-level table (bsgp_fft.hpp Tw2, 1.5 KiB) at the start of every
+  // kernel's LDS -- the full 32 KiB table does not fit beside the buffers, and
+  // from global memory every Stockham stage waited on an L2 round trip
+  if (g.coop && BSGP_COOP_TW2) {
+    size_t off = 0;
+    if (g.P == 2048) {
+      g.fp.lds_tw2 = 0;
+      off += (64 + 2048 / 64) * sizeof(cd);
+    }
+    if (g.Q == 2048) {
+      if (g.P == 2048) {
+        g.fq.lds_tw2 = 0;
+      } else {
+        g.fq.lds_tw2 = (int)off;
+        off += (64 + 2048 / 64) * sizeof(cd);
+      }
+    }
+    g.tw2 = (int)round_up(off, 16);
+    p->lds_bytes += g.tw2;
+  }
   if (!g.coop) {
     const size_t twb = (size_t)(g.P == g.Q ? g.P : g.P + g.Q) * sizeof(cd);
     if (p->lds_bytes + twb <= budget) {
@@ -590,7 +618,9 @@ int bsgp_plan_create_checked(int32_t H, int32_t W, const double* psf, int32_t kh
     p->pw.prog = p->pwprog;
   }
   if (hipMalloc(&p->active, 256) != hipSuccess ||
-      hipHostMalloc(&p->active_h, 256, hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc(&p->active_h, 256, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&p->done_h, 256, hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&p->done_d, p->done_h, 0) != hipSuccess) {
     bsgp_plan_destroy(p);
     return fail(BSGP_ERR_HIP, "counter allocation failed");
   }
@@ -612,6 +642,9 @@ int bsgp_plan_destroy(bsgp_plan p) {
   if (p->st) (void)hipFree(p->st);
   if (p->active) (void)hipFree(p->active);
   if (p->active_h) (void)hipHostFree(p->active_h);
+  if (p->done_h) (void)hipHostFree(p->done_h);
+  for (hipEvent_t e : p->ev_it)
+    if (e) (void)hipEventDestroy(e);
   if (p->opws) (void)hipFree(p->opws);
   if (p->tpart) (void)hipFree(p->tpart);
   if (p->tctr) (void)hipFree(p->tctr);
@@ -856,9 +889,12 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     }
     p->nsub = S;
   }
-  // device counter of running images: every setup block adds one, every
-  // stopping image subtracts one (k_bb)
-  HIP_TRY(hipMemsetAsync(p->active, 0, 16, s));
+  // device counter of images not yet stopped: B, counted down by every image
+  // the setup or k_bb stops (count_stopped); the last one writes this solve's
+  // seq to the host-mapped word
+  HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)p->active, B, 1, s));
+  a.seq = ++p->seq;
+  a.done_host = p->done_d;
   // team barrier counters and the timeout word restart at 0 every solve
   HIP_TRY(hipMemsetAsync(p->tctr, 0, p->tctr_bytes, s));
   hipStream_t ss[bsgp_plan_s::kMaxStreams];
@@ -911,9 +947,20 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     return BSGP_OK;
   }
   // Fixed-length runs (stop_criterion 0/1) are launched back to back with no
-  // host synchronisation; data-dependent stop rules poll the counter.
+  // host synchronisation.  Data-dependent stop rules are polled with
+  // lookahead: the host keeps at most kLook iterations queued ahead of the
+  // device (it waits for the event after iteration it - kLook, never for the
+  // stream to drain) and stops enqueueing once the host-mapped word carries
+  // this solve's seq, i.e. every image has stopped; the iterations queued
+  // past the last stop find every image stopped and return at once.  (Round 4
+  // drained the stream and copied the counter after EVERY iteration for
+  // B <= 4: one host round trip per iteration on the latency-bound
+  // single-image solves.)
   const bool data_stop = prm->stop_criterion >= 2 && prm->stop_criterion <= 4;
-  const int poll = data_stop ? (B <= 4 ? 1 : 4) : 0;
+  constexpr int kLook = 2;
+  if (data_stop)
+    for (int i = 0; i < bsgp_plan_s::kPollRing; ++i)
+      if (!p->ev_it[i]) HIP_TRY(hipEventCreateWithFlags(&p->ev_it[i], hipEventDisableTiming));
   int it_run = 0;
   for (int it = 1; it <= prm->MAXIT; ++it) {
     it_run = it;
@@ -922,11 +969,15 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
                                prof ? &prof->ev[2 + 6 * (size_t)(it - 1)] : nullptr));
       if (track) HIP_TRY(launch_track(sa[j], it, ss[j]));
     }
-    if (poll && it < prm->MAXIT && it % poll == 0) {
+    if (data_stop && it < prm->MAXIT && !BSGP_POLL_LOOKAHEAD) {  // (A/B: round 4's polling)
       for (int j = 0; j < S; ++j) HIP_TRY(hipStreamSynchronize(ss[j]));
-      HIP_TRY(hipMemcpyAsync(p->active_h, p->active, sizeof(int), hipMemcpyDeviceToHost, ss[0]));
-      HIP_TRY(hipStreamSynchronize(ss[0]));
-      if (*p->active_h <= 0) break;
+      if (__atomic_load_n(p->done_h, __ATOMIC_ACQUIRE) == a.seq) break;
+    } else if (data_stop && it < prm->MAXIT) {
+      HIP_TRY(hipEventRecord(p->ev_it[it % bsgp_plan_s::kPollRing], ss[0]));
+      if (it > kLook) {
+        HIP_TRY(hipEventSynchronize(p->ev_it[(it - kLook) % bsgp_plan_s::kPollRing]));
+        if (__atomic_load_n(p->done_h, __ATOMIC_ACQUIRE) == a.seq) break;
+      }
     }
   }
   if (S > 1) {

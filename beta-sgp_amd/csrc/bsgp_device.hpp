@@ -68,6 +68,8 @@ struct Geo {
   int coop;      // 1: thread groups of the workgroup run the transforms (long rows/columns)
   int lpad;      // complex elements per LDS buffer (odd: spreads banks)
   int sld;       // column stride of the stored half spectrum (>= H, even; BSGP_SPEC_PAD)
+  int tw2;       // bytes at the start of dynamic LDS holding two-level twiddle tables
+                 // (FftPlan::lds_tw2; cooperative 2048-point plans), else 0
   FftPlan fp;    // length P (columns)
   FftPlan fq;    // length Q (rows)
   const cd* tfA;   // [Qh][P] transfer function of A, scaled by 1/(P*Q)
@@ -88,9 +90,20 @@ __device__ __forceinline__ void copy_tw(const FftPlan& f) {
   cd* d = reinterpret_cast<cd*>(bsgp_dyn_lds + f.lds_tw);
   for (int i = threadIdx.x; i < f.n; i += kBlock) d[i] = f.tw[i];
 }
+// The two-level table (bsgp_fft.hpp Tw2) of a plan that placed one: entries
+// of the full global table, w^a (a < 64) then w^(64 b) (b < n/64).
+__device__ __forceinline__ void copy_tw2(const FftPlan& f) {
+  if (f.lds_tw2 < 0) return;
+  extern __shared__ __attribute__((aligned(16))) char bsgp_dyn_lds[];
+  cd* d = reinterpret_cast<cd*>(bsgp_dyn_lds + f.lds_tw2);
+  const int m = 64 + f.n / 64;
+  for (int i = threadIdx.x; i < m; i += blockDim.x) d[i] = f.tw[i < 64 ? i : 64 * (i - 64)];
+}
 __device__ __forceinline__ void load_tw_lds(const Geo& G) {
   copy_tw(G.fp);
   if (G.fq.lds_tw != G.fp.lds_tw) copy_tw(G.fq);
+  copy_tw2(G.fp);
+  if (G.fq.lds_tw2 != G.fp.lds_tw2) copy_tw2(G.fq);
   __syncthreads();
 }
 
@@ -751,6 +764,20 @@ __device__ __forceinline__ void coop_row_inv_fwd_1(const Geo& G, const Part& D, 
 #ifndef BSGP_COL_PAIR_NYQ
 #define BSGP_COL_PAIR_NYQ 1
 #endif
+// The column transforms' plan: BSGP_COL_TW2 0 (default) keeps them on the
+// global twiddle table, the row passes take the LDS two-level table.  With
+// the LDS table the column kernel needed 168 VGPRs (one 512-thread workgroup
+// per CU) or spilled at 128; on the global table it keeps two per CU.  C4 A/B
+// (profiles/r05/ab_round5.txt): global columns 1802 it/s, LDS columns at 128
+// VGPRs 1781, at 168 VGPRs 1770, no LDS table anywhere 1700.
+#ifndef BSGP_COL_TW2
+#define BSGP_COL_TW2 0
+#endif
+__device__ __forceinline__ FftPlan col_plan(const FftPlan& f) {
+  FftPlan c = f;
+  if (!BSGP_COL_TW2) c.lds_tw2 = -1;
+  return c;
+}
 __device__ __forceinline__ void coop_col_pair_nyq(const Geo& G, cd* spec, const cd* tf, cd* a,
                                                   cd* b) {
   const int t = threadIdx.x;
@@ -773,7 +800,7 @@ __device__ __forceinline__ void coop_col_pair_nyq(const Geo& G, cd* spec, const 
     }
   }
   __syncthreads();
-  cd* Z = fft_wide(a, b, G.fp, false, t, kBlock, BlockSync());
+  cd* Z = fft_wide(a, b, col_plan(G.fp), false, t, kBlock, BlockSync());
   cd* o = (Z == a) ? b : a;
   for (int p = t; p < G.P; p += kBlock) {
     cd A, B;
@@ -782,7 +809,7 @@ __device__ __forceinline__ void coop_col_pair_nyq(const Geo& G, cd* spec, const 
     o[p] = cmk(X.x - W.y, X.y + W.x);  // X + i W
   }
   __syncthreads();
-  cd* Y = fft_wide(o, Z, G.fp, true, t, kBlock, BlockSync());
+  cd* Y = fft_wide(o, Z, col_plan(G.fp), true, t, kBlock, BlockSync());
   for (int p = t; p < G.H; p += kBlock) {
     c0[p] = cmk(Y[p].x, 0.0);
     cN[p] = cmk(Y[p].y, 0.0);
@@ -819,7 +846,7 @@ __device__ __forceinline__ void coop_col_conv_1(const Geo& G, const Part& D, cd*
       }
     }
     __syncthreads();
-    cd* Z = fft_wide(a, b, G.fp, false, t, kBlock, BlockSync());
+    cd* Z = fft_wide(a, b, col_plan(G.fp), false, t, kBlock, BlockSync());
     for (int p0 = 0; p0 < G.P; p0 += kBlock * kCCH) {
       cd tv[kCCH];
 #pragma unroll
@@ -831,7 +858,7 @@ __device__ __forceinline__ void coop_col_conv_1(const Geo& G, const Part& D, cd*
       }
     }
     __syncthreads();
-    cd* Y = fft_wide(Z, (Z == a) ? b : a, G.fp, true, t, kBlock, BlockSync());
+    cd* Y = fft_wide(Z, (Z == a) ? b : a, col_plan(G.fp), true, t, kBlock, BlockSync());
     for (int p = t; p < G.H; p += kBlock) col[p] = Y[p];
     __syncthreads();
   }
@@ -1049,7 +1076,7 @@ __device__ __forceinline__ void coop_col_conv_g(const Geo& G, const Part& D, cd*
     __syncthreads();
     PH_ADD(29, tq0);
     PH_T(tq1);
-    cd* Z = fft_wide(a, b, G.fp, false, t, c.nt, BlockSync());
+    cd* Z = fft_wide(a, b, col_plan(G.fp), false, t, c.nt, BlockSync());
     if (act) {
       for (int p0 = 0; p0 < G.P; p0 += c.nt * kCCH) {
         cd tv[kCCH];
@@ -1063,7 +1090,7 @@ __device__ __forceinline__ void coop_col_conv_g(const Geo& G, const Part& D, cd*
       }
     }
     __syncthreads();
-    cd* Y = fft_wide(Z, (Z == a) ? b : a, G.fp, true, t, c.nt, BlockSync());
+    cd* Y = fft_wide(Z, (Z == a) ? b : a, col_plan(G.fp), true, t, c.nt, BlockSync());
     if (act)
       for (int p = t; p < G.H; p += c.nt) col[p] = Y[p];
     __syncthreads();

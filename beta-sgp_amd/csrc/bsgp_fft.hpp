@@ -53,6 +53,7 @@ struct FftPlan {
   int radix[kMaxStages];
   const cd* tw;  // n entries, exp(-2*pi*i*k/n)
   int lds_tw;    // device: byte offset of a copy of tw in dynamic LDS, or -1
+  int lds_tw2;   // device: byte offset of the two-level table (Tw2) in dynamic LDS, or -1
 };
 
 // Lengths with a compile-time transform (the hot grid sizes: 256 for circular
@@ -70,6 +71,22 @@ BSGP_HD bool fft_static_len(int n) {
 
 BSGP_HD cd tw_at(const cd* tw, int k, bool inv) {
   cd w = tw[k];
+  return inv ? cconj(w) : w;
+}
+
+// Two-level twiddle table of a length-n transform (n % 64 == 0, n <= 4096):
+// t1[a] = w^a (a < 64) and t2[b] = w^(64 b) (b < n/64), both entries of the
+// correctly rounded full table, so w^k = t1[k & 63] * t2[k >> 6] -- exact
+// where either factor is 1, within ~1 ulp elsewhere.  (64 + n/64) entries
+// (1.5 KiB for 2048) fit in LDS beside a workgroup-wide transform's buffers,
+// where the full table (32 KiB) does not: the twiddles of every stage come
+// from LDS instead of a global-memory round trip per stage.
+struct Tw2 {
+  const cd* t1;
+  const cd* t2;
+};
+BSGP_HD cd tw_at(const Tw2& t, int k, bool inv) {
+  const cd w = cmul(t.t1[k & 63], t.t2[k >> 6]);
   return inv ? cconj(w) : w;
 }
 
@@ -378,8 +395,8 @@ constexpr RadixList factor_radices(int n, bool comp = BSGP_FFT_COMPOSITE, bool r
   return L;
 }
 
-template <int R, int N, int Ns>
-BSGP_HD void stage_static(const cd* in, cd* out, const cd* tw, bool inv, int lane, int nlanes) {
+template <int R, int N, int Ns, class TW>
+BSGP_HD void stage_static(const cd* in, cd* out, TW tw, bool inv, int lane, int nlanes) {
   constexpr int nb = N / R;
   constexpr int twstep = N / (Ns * R);
 #pragma unroll 1
@@ -414,8 +431,8 @@ BSGP_HD void stage_static(const cd* in, cd* out, const cd* tw, bool inv, int lan
   }
 }
 
-template <int N, int S, int Ns, bool COMP, bool R8, class Sync>
-BSGP_HD cd* stages_static(cd* in, cd* out, const cd* tw, bool inv, int lane, int nlanes,
+template <int N, int S, int Ns, bool COMP, bool R8, class Sync, class TW>
+BSGP_HD cd* stages_static(cd* in, cd* out, TW tw, bool inv, int lane, int nlanes,
                           Sync sync) {
   constexpr RadixList L = factor_radices(N, COMP, R8);
   if constexpr (S < L.n) {
@@ -431,17 +448,29 @@ BSGP_HD cd* stages_static(cd* in, cd* out, const cd* tw, bool inv, int lane, int
 // Transform of compile-time length N (must be 2/3/5-smooth).  COMP: composite
 // radix-6/9 stages (fewer LDS round trips, ~20 more VGPRs live in the stage);
 // R8: radix-8 stages first (for 256-lane workgroup transforms).
-template <int N, bool COMP = BSGP_FFT_COMPOSITE, bool R8 = false, class Sync>
-BSGP_HD cd* fft_run_static(cd* a, cd* b, const cd* tw, bool inv, int lane, int nlanes, Sync sync) {
+template <int N, bool COMP = BSGP_FFT_COMPOSITE, bool R8 = false, class Sync, class TW>
+BSGP_HD cd* fft_run_static(cd* a, cd* b, TW tw, bool inv, int lane, int nlanes, Sync sync) {
   static_assert(factor_radices(N).n > 0, "N must be 2/3/5-smooth");
   return stages_static<N, 0, 1, COMP, R8>(a, b, tw, inv, lane, nlanes, sync);
 }
+
+#if defined(__HIP_DEVICE_COMPILE__)
+extern __shared__ __attribute__((aligned(16))) char bsgp_dyn_lds[];
+#endif
 
 // Workgroup-wide transform (all kBlock-style lanes, `sync` = workgroup
 // barrier): compile-time radix-8 plan for 2048 (config C4), runtime plan otherwise.
 template <class Sync>
 BSGP_HD cd* fft_wide(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlanes, Sync sync) {
-  if (p.n == 2048) return fft_run_static<2048, true, true>(a, b, p.tw, inv, lane, nlanes, sync);
+  if (p.n == 2048) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (p.lds_tw2 >= 0) {  // the two-level table in LDS (bsgp_plan_create, load_tw_lds)
+      const cd* t = reinterpret_cast<const cd*>(bsgp_dyn_lds + p.lds_tw2);
+      return fft_run_static<2048, true, true>(a, b, Tw2{t, t + 64}, inv, lane, nlanes, sync);
+    }
+#endif
+    return fft_run_static<2048, true, true>(a, b, p.tw, inv, lane, nlanes, sync);
+  }
   return fft_run(a, b, p, inv, lane, nlanes, sync);
 }
 
@@ -449,9 +478,6 @@ BSGP_HD cd* fft_wide(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nla
 // device every transform reads its twiddles from the LDS copy the kernel made
 // when the plan placed one (plan.lds_tw >= 0; LDS latency instead of L1/L2
 // latency in every butterfly round), else the global table.
-#if defined(__HIP_DEVICE_COMPILE__)
-extern __shared__ __attribute__((aligned(16))) char bsgp_dyn_lds[];
-#endif
 template <bool COMP = BSGP_FFT_COMPOSITE, class Sync>
 BSGP_HD cd* fft_any(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlanes, Sync sync) {
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -64,7 +64,11 @@ struct SolveArgs {
   int B;
   int img0, nimg;      // this launch's sub-batch [img0, img0 + nimg)
   ImgState* st;        // [B]
-  int* active;         // images still iterating
+  int* active;         // images not yet stopped: B at the start (the host sets it); the setup
+                       // and k_bb count each stopping image down
+  int* done_host;      // host-mapped word: the solve's `seq` once `active` reaches 0 (the
+                       // host's lookahead polling of data-dependent stop rules), or nullptr
+  int seq;             // this solve's sequence number (done_host)
   double* ws;          // per-image slots
   size_t slot_stride;  // doubles per slot
   size_t vec_stride;   // doubles per image vector (N rounded up to 32)
@@ -156,6 +160,12 @@ void persist_kernels_all(std::vector<const void*>& f);
 #endif
 #ifndef BSGP_COOP_GROUPS
 #define BSGP_COOP_GROUPS 4
+#endif
+#ifndef BSGP_POLL_LOOKAHEAD
+#define BSGP_POLL_LOOKAHEAD 1  // data-dependent stop rules: lookahead polling (bsgp_api.hip)
+#endif
+#ifndef BSGP_COOP_TW2
+#define BSGP_COOP_TW2 1  // two-level LDS twiddles for cooperative 2048-point transforms
 #endif
 #ifndef BSGP_SPEC_PAD
 #define BSGP_SPEC_PAD 0  // rows of padding per stored spectrum column (even)

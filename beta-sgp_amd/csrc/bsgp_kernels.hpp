@@ -324,8 +324,8 @@ __device__ __forceinline__ bool leader(const Team& t) { return t.m == 0 && threa
 
 #define BSGP_LDS_VIEWS(A)                                                           \
   extern __shared__ __attribute__((aligned(16))) char smem[];                      \
-  cd* lds = reinterpret_cast<cd*>(smem);                                           \
-  double* red = reinterpret_cast<double*>(smem + (A).lds_fft_bytes)
+  cd* lds = reinterpret_cast<cd*>(smem + (A).g.tw2);                               \
+  double* red = reinterpret_cast<double*>(smem + (A).g.tw2 + (A).lds_fft_bytes)
 
 // numpy's float32 np.sum of term(i) for i < N, in numpy's exact order (the
 // plan's PwProg, bsgp_api.hip pairwise_program): the leaves by the team's
@@ -402,6 +402,15 @@ __device__ __forceinline__ void write_counters(const SolveArgs& A, const ImgStat
   c[5] = T;
   c[6] = st.proj_passes;
   c[7] = st.proj_list;
+}
+
+// An image stopped: count it down; the one that takes the count to 0 tells
+// the host (a system-scope vector store to host-mapped memory, read after an
+// event the host waits on), so the host need not drain the stream to learn
+// that every image has stopped.
+__device__ __forceinline__ void count_stopped(const SolveArgs& A) {
+  if (atomicSub(A.active, 1) == 1 && A.done_host)
+    __hip_atomic_store(A.done_host, A.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ------------------------------------------------------------ kernel: setup
@@ -659,8 +668,7 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
       A.out.iters[img] = 0;
       if (A.out.beta_final) A.out.beta_final[img] = st.beta;
       write_counters(A, st, img, tm.T);
-    } else {
-      atomicAdd(A.active, 1);
+      count_stopped(A);
     }
   }
 }
@@ -1399,6 +1407,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_LS_ATTR k_ls(SolveArgs A) {
   ls_phase<K, MODE, ADAPT, COOP, V>(A, img);
 }
 
+
 // ------------------------------ kernel: gradient, x update, BB, stop rules
 // sgp.py:337-414 (= 785-879): g_new = g1(den) - AT(w), x += lam*d, the
 // Barzilai-Borwein step lengths with the tau alternation, the stop rules,
@@ -1532,7 +1541,7 @@ __device__ __forceinline__ void bb_phase(const SolveArgs& A, int img) {
       A.out.iters[img] = it2 - 1;
       if (A.out.beta_final) A.out.beta_final[img] = st.beta;
       write_counters(A, st, img, tm.T);
-      atomicSub(A.active, 1);
+      count_stopped(A);
     }
   }
 }
@@ -1972,7 +1981,7 @@ inline hipError_t launch_iteration_t(const SolveArgs& a, int K, size_t lds, hipS
 #define BSGP_COL_LDS_FULL 0
 #endif
   const size_t lds_col =
-      (COOP && !BSGP_COL_LDS_FULL) ? (size_t)a.g.nfc * 2 * a.g.lpad * sizeof(cd) : lds;
+      (COOP && !BSGP_COL_LDS_FULL) ? (size_t)a.g.nfc * 2 * a.g.lpad * sizeof(cd) + a.g.tw2 : lds;
   if (!(a.fuse_col & 5)) chk(launch_fn((const void*)k_col<COOP>, gcol, lds_col, s, a, 0));
   if (ev) chk(hipEventRecord(ev[2], s));
   // line-search kernel specialised on trial width, objective mode, adaptivity

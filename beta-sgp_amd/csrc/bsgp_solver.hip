@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(kBlock) tf_rows_kernel(Geo G, const double* kc
                                                          size_t kc_stride, cd* spec,
                                                          size_t spec_stride) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  cd* lds = reinterpret_cast<cd*>(smem);
+  cd* lds = reinterpret_cast<cd*>(smem + G.tw2);
   kc += blockIdx.y * kc_stride;
   spec += blockIdx.y * spec_stride;
   load_tw_lds(G);
@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(kBlock) tf_cols_kernel(Geo G, const cd* spec,
                                                          size_t tf_stride, double scale,
                                                          int conj) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  cd* lds = reinterpret_cast<cd*>(smem);
+  cd* lds = reinterpret_cast<cd*>(smem + G.tw2);
   spec += blockIdx.y * spec_stride;
   tf += blockIdx.y * tf_stride;
   load_tw_lds(G);
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(kBlock) apply_op_kernel(Geo G, int B, int tran
                                                           const double* x, double* out,
                                                           cd* specws, size_t spec_stride) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  cd* lds = reinterpret_cast<cd*>(smem);
+  cd* lds = reinterpret_cast<cd*>(smem + G.tw2);
   const int N = G.H * G.W;
   cd* spec = specws + (size_t)blockIdx.x * spec_stride;
   load_tw_lds(G);
@@ -184,7 +184,7 @@ template <bool COOP>
 __global__ void __launch_bounds__(kBlock) op_rows_kernel(Geo G, const double* x, cd* specws,
                                                          size_t spec_stride) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  cd* lds = reinterpret_cast<cd*>(smem);
+  cd* lds = reinterpret_cast<cd*>(smem + G.tw2);
   const double* xi = x + (size_t)blockIdx.y * G.H * G.W;
   Part D = solo_part(G.nfw);
   D.gw0 = blockIdx.x * G.nfw;
@@ -197,7 +197,7 @@ template <bool COOP>
 __global__ void __launch_bounds__(kBlock) op_cols_kernel(Geo G, int transpose, cd* specws,
                                                          size_t spec_stride) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  cd* lds = reinterpret_cast<cd*>(smem);
+  cd* lds = reinterpret_cast<cd*>(smem + G.tw2);
   Part D = solo_part(G.nfw);
   D.gw0 = blockIdx.x * G.nfw;
   D.gws = gridDim.x * G.nfw;
@@ -208,7 +208,7 @@ template <bool COOP>
 __global__ void __launch_bounds__(kBlock) op_rows_inv_kernel(Geo G, cd* specws,
                                                              size_t spec_stride, double* out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  cd* lds = reinterpret_cast<cd*>(smem);
+  cd* lds = reinterpret_cast<cd*>(smem + G.tw2);
   double* oi = out + (size_t)blockIdx.y * G.H * G.W;
   Part D = solo_part(G.nfw);
   D.gw0 = blockIdx.x * G.nfw;

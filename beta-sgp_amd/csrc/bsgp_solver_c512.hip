@@ -21,6 +21,15 @@
 
 #define BSGP_BLOCK 512
 #define bsgp bsgp_c512
+// the column kernel keeps two 512-thread workgroups per CU (<= 128 VGPRs): its
+// LDS (two 2048-point buffers + the two-level twiddles, 67 KiB) holds two, and
+// the twiddle products of the LDS table had taken it to 168 VGPRs (one per CU)
+#ifndef BSGP_COL_WPE
+#define BSGP_COL_WPE 4
+#endif
+#if BSGP_COL_WPE
+#define BSGP_COL_ATTR __attribute__((amdgpu_waves_per_eu(BSGP_COL_WPE)))
+#endif
 #include "bsgp_kernels.hpp"
 
 namespace bsgp {

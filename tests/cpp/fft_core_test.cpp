@@ -140,6 +140,23 @@ int main() {
         bad++;
       }
     }
+    {  // the two-level twiddle table (Tw2: w^a * w^(64 b), the device's LDS copy)
+      std::vector<cd> t2(64 + n / 64);
+      for (int a = 0; a < 64; ++a) t2[a] = tw[a];
+      for (int b2 = 0; b2 < n / 64; ++b2) t2[64 + b2] = tw[64 * b2];
+      std::vector<cd> x(c), y(n);
+      cd* r3 = fft_run_static<2048, true, true>(x.data(), y.data(), Tw2{t2.data(), t2.data() + 64},
+                                               inv, 0, 1, [] {});
+      double maxdiff = 0, maxref = 0;
+      for (int k = 0; k < n; ++k) {
+        maxdiff = fmax(maxdiff, fabs(r1[k].x - r3[k].x) + fabs(r1[k].y - r3[k].y));
+        maxref = fmax(maxref, fabs(r1[k].x) + fabs(r1[k].y));
+      }
+      if (!(maxdiff / maxref < 1e-14)) {
+        printf("FAIL wide n=2048 two-level twiddles inv=%d diff %g\n", inv, maxdiff / maxref);
+        bad++;
+      }
+    }
   }
   printf(bad ? "FFT core: %d failures\n" : "FFT core: all ok\n", bad);
   return bad ? 1 : 0;
