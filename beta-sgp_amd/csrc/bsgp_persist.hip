@@ -15,7 +15,7 @@ namespace bsgp {
 
 hipError_t launch_persist_f32(const SolveArgs& a, int K, size_t lds, hipStream_t s,
                               unsigned* queue, unsigned* done, int grid);
-const void* persist_kernel_f32(int K, int mode, bool adapt);
+const void* persist_kernel_f32(int K, int mode, bool adapt, bool scalar_bkg);
 void persist_kernels_f32(std::vector<const void*>& f);
 
 static int persist_mode(const SolveArgs& a, bool* adapt) {
@@ -40,8 +40,9 @@ hipError_t persist_resident_per_cu(const SolveArgs& a, int K, size_t lds, int* p
   if (app_static_plan(a.g, a.storage)) return bsgp_app_persist_resident(&a, K, lds, per_cu);
   bool adapt = false;
   const int mode = persist_mode(a, &adapt);
-  const void* f = a.storage == BSGP_STORAGE_F32 ? persist_kernel_f32(K, mode, adapt)
-                                                : persist_kernel<double>(K, mode, adapt);
+  const bool sb = !a.prm.bkg_is_map;
+  const void* f = a.storage == BSGP_STORAGE_F32 ? persist_kernel_f32(K, mode, adapt, sb)
+                                                : persist_kernel<double>(K, mode, adapt, sb);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, f, kBlock, lds);
 }
 

@@ -59,7 +59,8 @@ hipError_t bsgp_app_persist_resident(const void* a, int K, size_t lds, int* per_
   bool adapt = false;
   const int mode = bsgp_app::persist_mode_app(A, &adapt);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      per_cu, bsgp_app::persist_kernel<double>(K, mode, adapt), bsgp_app::kBlock, lds);
+      per_cu, bsgp_app::persist_kernel<double>(K, mode, adapt, !A.prm.bkg_is_map),
+      bsgp_app::kBlock, lds);
 }
 
 hipError_t bsgp_app_persist_set_lds_limit(size_t bytes) {

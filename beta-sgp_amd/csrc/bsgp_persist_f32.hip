@@ -12,8 +12,8 @@ hipError_t launch_persist_f32(const SolveArgs& a, int K, size_t lds, hipStream_t
                               unsigned* queue, unsigned* done, int grid) {
   return launch_persist_t<float>(a, K, lds, s, queue, done, grid);
 }
-const void* persist_kernel_f32(int K, int mode, bool adapt) {
-  return persist_kernel<float>(K, mode, adapt);
+const void* persist_kernel_f32(int K, int mode, bool adapt, bool scalar_bkg) {
+  return persist_kernel<float>(K, mode, adapt, scalar_bkg);
 }
 void persist_kernels_f32(std::vector<const void*>& f) { persist_kernels<float>(f); }
 hipError_t persist_phase_prof_f32(unsigned long long* out, int n, int reset) {

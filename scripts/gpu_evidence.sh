@@ -2,7 +2,7 @@
 # Evidence from ONE lease: smoke, PMC traffic (two passes) copied to
 # profiles/traffic_c3.json, the default bench line (C3) that reads it, the
 # rocprofv3 kernel statistics of the same command, SQ counters of k_persist,
-# and the other configuration lines.  Usage: bash scripts/gpu_r04_evidence.sh TAG
+# and the other configuration lines.  Usage: bash scripts/gpu_evidence.sh TAG
 set -o pipefail
 TAG=${1:-ev}
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/$TAG; export TMPDIR=/tmp
@@ -31,8 +31,8 @@ for C in "$P1" "$P2"; do
   S=$(find $O/sq_p$i -name "*counter_collection.csv" | head -1)
   python tools/pmc_summary.py $S | grep -E "k_persist" | tee $O/sq_p$i.txt
 done
-for cfg in "stamps31" "sub375" "sub450" "c5" "c2" "c4 --storage f32" "c4"; do
+for cfg in "stamps31" "stamps31_kl" "app375" "sub375" "sub450" "c5" "c2" "c4 --storage f32" "c4"; do
   name=$(echo $cfg | tr ' ' '_' | tr -d '-')
   timeout -k 10 400 python bench.py --config $cfg > $O/bench_$name.json 2> $O/bench_$name.err || { echo "bench $cfg failed"; tail -5 $O/bench_$name.err; exit 3; }
-  python -c "import json;d=json.load(open('$O/bench_$name.json'));r=d['roofline'] or {};c=d.get('cpu_baseline') or {};print('$name', round(d['value']), 'frac', round(r.get('frac',0),3), 'solve', round(r.get('solve',{}).get('frac_timed',0),3), 'cpu', round(c.get('value',0),1))"
+  python -c "import json;d=json.load(open('$O/bench_$name.json'));r=d['roofline'] or {};c=d.get('cpu_baseline') or {};print('$name', round(d['value']), 'frac', round(r.get('frac') or 0,3), 'solve', round((r.get('solve') or {}).get('frac_timed',0),3), 'cpu', round(c.get('value') or 0,1))"
 done
