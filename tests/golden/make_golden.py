@@ -585,7 +585,9 @@ def make_c4():
     astropy).  The input is rebuilt by oracle/cpu_bench.make_stamp(0, 2048,
     64, 5000, circular=True) wherever the fixture is used, so only the
     outputs are stored: the discrepancy and trial count of every iteration,
-    sum(x), the flux-weighted centroid, and four 64x64 windows of x."""
+    sum(x), sum(x^2), four 64x64 windows of x in float64, and the whole
+    field x rounded to float32 (x32: a per-pixel pin of the float64 path to
+    about 1e-7 without shipping 32 MiB of float64)."""
     sgp, fcp = import_reference(need_astropy=False)
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(OUT)), "oracle"))
     import cpu_bench
@@ -601,6 +603,7 @@ def make_c4():
                fn="sgp_betaDiv")
     for j, (r, c) in enumerate(wins):
         out[f"win{j}"] = x[r:r + 64, c:c + 64]
+    out["x32"] = x.astype(np.float32)
     np.savez_compressed(os.path.join(OUT, "ref_c4_maxit20.npz"), **out)
     print("c4 iters", it, "trials", trials.sum(), "discrN", discr[-1])
 
