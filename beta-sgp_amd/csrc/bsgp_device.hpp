@@ -25,6 +25,22 @@ namespace bsgp {
 constexpr int kBlock = BSGP_BLOCK;  // threads per workgroup (one image per workgroup)
 constexpr int kWaves = kBlock / 64;
 constexpr int kMaxRed = 24;  // doubles reduced at once
+
+// Team barriers and reductions on per-member words (round 5)
+// for teams of at most BSGP_TEAM_FLAGS members: a member's arrival is one
+// store to its own word and its reduction partials are their own arrival
+// flags (slots pre-filled with kPartEmpty, triple-buffered), so a barrier is
+// one store plus the readers' polls instead of the hierarchical counters'
+// chain of atomics.  Every member polls every member, so larger teams (C4's
+// 256) keep the XCD-hierarchical counters; 0 disables the flags (A/B).
+#ifndef BSGP_TEAM_FLAGS
+#define BSGP_TEAM_FLAGS 64
+#endif
+constexpr int kPartBufs = 3;
+// A signalling NaN (hi word == lo word, so hipMemsetD32 can fill it):
+// arithmetic never produces one, and stored partials are canonicalised.
+constexpr unsigned long long kPartEmpty = 0xFFF75EE0FFF75EE0ull;
+constexpr unsigned int kPartEmptyWord = 0xFFF75EE0u;
 constexpr int kSharedBytes = 512;  // LDS after the wave partials: reduced totals + scalars
 
 // Phase profile (builds with -DBSGP_PHASE_PROF only): thread 0 of every
@@ -227,7 +243,8 @@ constexpr int kTeamWords = 17 * kTeamLine;
 
 struct Team {
   int m, T;            // member index, team size
-  double* part;        // [2][T][kMaxRed] partial slots of this image (double-buffered)
+  double* part;        // [3][T][kMaxRed] partial slots of this image
+  bool flags;          // flag barriers (T <= BSGP_TEAM_FLAGS), else counters
   unsigned int* ctr;   // the image's kTeamWords barrier words (monotonic across kernels)
   unsigned int base;   // barriers the team completed before this kernel (same in all members)
   int nb;              // team barriers passed in this kernel
@@ -314,6 +331,50 @@ __device__ __forceinline__ void team_arrive_wait(Team& t) {
   }
 }
 
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__device__ __forceinline__ bool part_empty(double v) {
+  return (unsigned long long)__double_as_longlong(v) == kPartEmpty;
+}
+
+// Flag barriers.  Every barrier of a solve (data or reduction) has a global
+// number g = base + nb, the same in every member.  Data barrier g: member m
+// stores g + 1 to its arrival word ctr[m] after a release and polls every
+// member's word.  Reduction g: member m stores its partials to slot g % 3
+// (which holds kPartEmpty) and polls every member's partials of that slot
+// until none is empty.  After barrier g a member refills its own slot
+// (g + 2) % 3, which held barrier g - 1's partials: every member has read
+// those, since every member has arrived at g.  The refill completes before
+// the member's next arrival (both are wave 0's, behind an s_waitcnt), so no
+// member can see a stale partial in a slot it polls.
+__device__ __forceinline__ double* team_slot(const Team& t, unsigned int ahead) {
+  return t.part + (size_t)((t.base + (unsigned int)t.nb + ahead) % 3u) * t.T * kMaxRed;
+}
+__device__ __forceinline__ void team_refill(const Team& t) {
+  if (threadIdx.x < kMaxRed)
+    __hip_atomic_store((gu64*)(team_slot(t, 2) + (size_t)t.m * kMaxRed + threadIdx.x), kPartEmpty,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// wave 0: until every member's arrival word is >= n1
+__device__ __forceinline__ void team_wait_words(Team& t, unsigned int n1) {
+  unsigned int spins = 0;
+  for (;;) {
+    bool ok = true;
+    for (int mm = (int)threadIdx.x; mm < t.T; mm += 64)
+      ok &= (int)(__hip_atomic_load((gu32*)(t.ctr + mm), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) - n1) >= 0;
+    if (__all(ok)) return;
+    if (!team_spin(t, spins)) return;
+  }
+}
+
 // Data barrier: everything any member stored before it is visible to every
 // member after it.
 __device__ __forceinline__ void team_sync(Team& t) {
@@ -323,7 +384,22 @@ __device__ __forceinline__ void team_sync(Team& t) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (t.flags) {
+    if (threadIdx.x < 64) {
+      const unsigned int n1 = t.base + (unsigned int)t.nb + 1;
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store((gu32*)(t.ctr + t.m), n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      team_wait_words(t, n1);
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      team_refill(t);
+    }
+  } else if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     team_arrive_wait(t);
@@ -334,26 +410,50 @@ __device__ __forceinline__ void team_sync(Team& t) {
   t.nb += 1;
 }
 
-// Reduction barrier: thread 0 has stored this member's partials with sc1
-// stores; drain them, arrive, wait.  The partials are then read with sc1
-// loads (no acquire needed: nothing else crosses workgroups here).
+// Reduction barrier (counters): thread 0 has stored this member's partials
+// with sc1 stores; drain them, arrive, wait.  The partials are then read
+// with sc1 loads (no acquire needed: nothing else crosses workgroups here).
+// With flag barriers the partials are the arrival: nothing to do here.
 __device__ __forceinline__ void team_red_barrier(Team& t) {
+  if (t.flags) return;
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     team_arrive_wait(t);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
   }
   __syncthreads();
+}
+// After the totals are read: with flag barriers refill the slot two
+// barriers ahead; count the barrier.
+__device__ __forceinline__ void team_red_done(Team& t) {
+  if (t.flags && threadIdx.x < 64) team_refill(t);
   t.nb += 1;
 }
-
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+// This barrier's partial slots.
+__device__ __forceinline__ double* red_slot(const Team& t) {
+  return t.flags ? team_slot(t, 0) : t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
 }
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __longlong_as_double(
-      (long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+// Wave 0's poll over the partials: with flag barriers the loads repeat until
+// no partial is empty; otherwise one pass.
+__device__ __forceinline__ bool red_poll_done(Team& t, bool ok, unsigned int& spins) {
+  if (!t.flags || __all(ok)) return true;
+  return !team_spin(t, spins);
+}
+// Wide flag reductions (more than BSGP_RED_POLL_MAX loads per lane: NV + NM
+// values of ceil(T / 64) members): poll one value per member, the last one
+// stored, before loading all of them, so a poll round is one load per member.
+#ifndef BSGP_RED_POLL_MAX
+#define BSGP_RED_POLL_MAX 24
+#endif
+__device__ __forceinline__ void red_wait_last(Team& t, const double* slot, int last) {
+  if (!t.flags || (last + 1) * ((t.T + 63) >> 6) <= BSGP_RED_POLL_MAX) return;
+  unsigned int spins = 0;
+  for (;;) {
+    bool ok = true;
+    for (int mm = (int)threadIdx.x; mm < t.T; mm += 64)
+      ok &= !part_empty(ld_sc1(slot + (size_t)mm * kMaxRed + last));
+    if (red_poll_done(t, ok, spins)) return;
+  }
 }
 
 // A member's block totals of NV sums and NM maxima, stored straight to its
@@ -390,6 +490,8 @@ __device__ __forceinline__ void member_partials(const double* v, const double* m
         s = (u > s || u != u) ? u : s;
       }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's refills first (flags)
+    if (s != s) s = __longlong_as_double(0x7ff8000000000000ll);  // never kPartEmpty
     st_sc1(dst + i, s);
   }
 }
@@ -401,7 +503,7 @@ __device__ __forceinline__ void team_sum(double (&v)[NV], double* red, Team& t) 
     block_sum<NV>(v, red);
     return;
   }
-  double* slot = t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
+  double* slot = red_slot(t);
   const double none[1] = {0.0};
   member_partials<NV, 0>(v, none, red, slot + (size_t)t.m * kMaxRed);
   team_red_barrier(t);
@@ -410,12 +512,22 @@ __device__ __forceinline__ void team_sum(double (&v)[NV], double* red, Team& t) 
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     double s[NV];
+    unsigned int spins = 0;
+    red_wait_last(t, slot, NV - 1);
+    for (;;) {
+      bool ok = true;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) s[i] = 0.0;
-    for (int mm = lane; mm < t.T; mm += 64) {
-      const double* q = slot + (size_t)mm * kMaxRed;
+      for (int i = 0; i < NV; ++i) s[i] = 0.0;
+      for (int mm = lane; mm < t.T; mm += 64) {
+        const double* q = slot + (size_t)mm * kMaxRed;
 #pragma unroll
-      for (int i = 0; i < NV; ++i) s[i] += ld_sc1(q + i);
+        for (int i = 0; i < NV; ++i) {
+          const double u = ld_sc1(q + i);
+          ok &= !part_empty(u);
+          s[i] += u;
+        }
+      }
+      if (red_poll_done(t, ok, spins)) break;
     }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
@@ -427,6 +539,7 @@ __device__ __forceinline__ void team_sum(double (&v)[NV], double* red, Team& t) 
 #pragma unroll
   for (int i = 0; i < NV; ++i) v[i] = red[kWaves * kMaxRed + i];
   __syncthreads();
+  team_red_done(t);
 }
 
 // NV sums and NM maxima in ONE team barrier (NaN propagates through the
@@ -444,25 +557,36 @@ __device__ __forceinline__ void team_reduce(double (&v)[NV > 0 ? NV : 1], double
     for (int k = 0; k < NM; ++k) mx[k] = block_max(mx[k], red);
     return;
   }
-  double* slot = t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
+  double* slot = red_slot(t);
   member_partials<NV, NM>(v, mx, red, slot + (size_t)t.m * kMaxRed);
   team_red_barrier(t);
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     double s[NV + 1], m[NM];
+    unsigned int spins = 0;
+    red_wait_last(t, slot, NV + NM - 1);
+    for (;;) {
+      bool ok = true;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) s[i] = 0.0;
+      for (int i = 0; i < NV; ++i) s[i] = 0.0;
 #pragma unroll
-    for (int k = 0; k < NM; ++k) m[k] = -INFINITY;
-    for (int mm = lane; mm < t.T; mm += 64) {
-      const double* q = slot + (size_t)mm * kMaxRed;
+      for (int k = 0; k < NM; ++k) m[k] = -INFINITY;
+      for (int mm = lane; mm < t.T; mm += 64) {
+        const double* q = slot + (size_t)mm * kMaxRed;
 #pragma unroll
-      for (int i = 0; i < NV; ++i) s[i] += ld_sc1(q + i);
+        for (int i = 0; i < NV; ++i) {
+          const double u = ld_sc1(q + i);
+          ok &= !part_empty(u);
+          s[i] += u;
+        }
 #pragma unroll
-      for (int k = 0; k < NM; ++k) {
-        const double u = ld_sc1(q + NV + k);
-        m[k] = (u > m[k] || u != u) ? u : m[k];
+        for (int k = 0; k < NM; ++k) {
+          const double u = ld_sc1(q + NV + k);
+          ok &= !part_empty(u);
+          m[k] = (u > m[k] || u != u) ? u : m[k];
+        }
       }
+      if (red_poll_done(t, ok, spins)) break;
     }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
@@ -481,6 +605,7 @@ __device__ __forceinline__ void team_reduce(double (&v)[NV > 0 ? NV : 1], double
 #pragma unroll
   for (int k = 0; k < NM; ++k) mx[k] = red[kWaves * kMaxRed + NV + k];
   __syncthreads();
+  team_red_done(t);
 }
 template <int NV>
 __device__ __forceinline__ void team_sum_max(double (&v)[NV], double& mx, double* red, Team& t) {
@@ -494,15 +619,26 @@ template <bool MAX>
 __device__ __forceinline__ double team_ext(double v, double* red, Team& t) {
   v = MAX ? block_max(v, red) : block_min(v, red);
   if (t.T == 1) return v;
-  double* slot = t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
-  if (threadIdx.x == 0) st_sc1(slot + (size_t)t.m * kMaxRed, v);
+  double* slot = red_slot(t);
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's refills first (flags)
+    if (v != v) v = __longlong_as_double(0x7ff8000000000000ll);  // never kPartEmpty
+    st_sc1(slot + (size_t)t.m * kMaxRed, v);
+  }
   team_red_barrier(t);
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    double s = MAX ? -INFINITY : INFINITY;
-    for (int mm = lane; mm < t.T; mm += 64) {
-      const double u = ld_sc1(slot + (size_t)mm * kMaxRed);
-      s = MAX ? ((u > s || u != u) ? u : s) : ((u < s || u != u) ? u : s);
+    double s;
+    unsigned int spins = 0;
+    for (;;) {
+      bool ok = true;
+      s = MAX ? -INFINITY : INFINITY;
+      for (int mm = lane; mm < t.T; mm += 64) {
+        const double u = ld_sc1(slot + (size_t)mm * kMaxRed);
+        ok &= !part_empty(u);
+        s = MAX ? ((u > s || u != u) ? u : s) : ((u < s || u != u) ? u : s);
+      }
+      if (red_poll_done(t, ok, spins)) break;
     }
     s = MAX ? wave_max(s) : wave_min(s);
     if (lane == 0) red[kWaves * kMaxRed] = s;
@@ -510,6 +646,7 @@ __device__ __forceinline__ double team_ext(double v, double* red, Team& t) {
   __syncthreads();
   const double r = red[kWaves * kMaxRed];
   __syncthreads();
+  team_red_done(t);
   return r;
 }
 __device__ __forceinline__ double team_max(double v, double* red, Team& t) {

@@ -77,7 +77,7 @@ struct SolveArgs {
   int T;
   int Tc;               // workgroups per image of k_col (no reductions there: not a team)
   int fuse_col;         // T == 1: BSGP_FUSE_COL (which phase kernels run the column passes)
-  double* tpart;        // [B][2][T][kMaxRed] reduction partials
+  double* tpart;        // [B][kPartBufs][T][kMaxRed] reduction partials
   unsigned int* tctr;   // [B][kTeamWords] barrier words, then the timeout word; zeroed per solve
   int* tfail;           // set by a timed-out barrier spin
   // projection pixel lists (proj_cache): per image two arrays (y, X) of
