@@ -843,6 +843,7 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   a.plist = nullptr;
   a.plist_stride = 0;
   a.lcap = 0;
+  a.list_lds = 0;
   a.pw = p->pw;
   a.storage = p->storage;
   a.spec_off = p->spec_off;
@@ -857,6 +858,10 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     rc = ensure_plist(p, (size_t)B * a.plist_stride);
     if (rc) return rc;
     a.plist = p->plist;
+    a.list_lds = (BSGP_LIST_LDS && T > 1 &&
+                  (size_t)a.lcap * plan_block(p->g) * 2 * sizeof(double) <= p->lds_fft_bytes)
+                     ? 1
+                     : 0;
   }
   hipStream_t s = (hipStream_t)stream;
   const int K = (prm->adapt_beta && prm->variant == BSGP_VARIANT_BETA)

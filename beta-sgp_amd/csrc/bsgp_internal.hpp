@@ -47,6 +47,10 @@ struct ImgState {
 // fused-column code compiled into the kernels (a pass not compiled in costs no
 // registers in the kernels that never run it)
 #define BSGP_FUSE_COL_CODE (BSGP_FUSE_COL | BSGP_FUSE_COL_TEAM)
+// teams keep their projection lists in LDS when they fit (0: global, A/B)
+#ifndef BSGP_LIST_LDS
+#define BSGP_LIST_LDS 1
+#endif
 
 // numpy float32 reduction program of a plan's N (bsgp_api.hip pairwise_program):
 // [nleaf][2] leaves (start, len), [nnode][2] node operands (value indices),
@@ -85,6 +89,7 @@ struct SolveArgs {
   double* plist;
   size_t plist_stride;  // doubles per image (both arrays)
   int lcap;             // list capacity per thread (pixels one thread streams)
+  int list_lds;         // teams: the lists live in the transform buffers' LDS
   PwProg pw;            // numpy float32 sum order over N (params.gn_f32)
   int storage;          // BSGP_STORAGE_F64 / F32 (iteration vectors, Bufs<V>)
   size_t spec_off;      // doubles from a slot's start to its spectrum

@@ -708,11 +708,15 @@ constexpr double kProjGuessW = BSGP_PROJ_GUESS_W;
 #define BSGP_PROJ_WIDE_PX 16
 #endif
 
-template <class V>
+// Teams whose lists fit the transform buffers (SolveArgs::list_lds: C2, the
+// application's subdivisions) keep them in LDS, which the row pass after the
+// projection is the next to use: an evaluation then reads no global memory
+// (LL: compiled in; the persistent one-workgroup solver keeps global lists).
+template <class V, bool LL>
 __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt, Team& tm,
-                                     const Dir& D, const Bufs<V>& B, double* red, double lam_prev,
-                                     double flux, int npair, bool odd, int N, int64_t& passes,
-                                     int64_t& list_reads) {
+                                     const Dir& D, const Bufs<V>& B, double* red, cd* lds,
+                                     double lam_prev, double flux, int npair, bool odd, int N,
+                                     int64_t& passes, int64_t& list_reads) {
   const V* xa = B.xa;
   const V* ga = B.ga;
   const int LS = tm.T * kBlock;
@@ -720,6 +724,10 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
   double* ly = A.plist + (size_t)img * A.plist_stride;
   double* lX = ly + A.plist_stride / 2;
   const int lcap = A.lcap;
+  const bool lds_list = LL && A.list_lds != 0;
+  double* const qy = reinterpret_cast<double*>(lds);
+  double* const qX = qy + (size_t)lcap * kBlock;
+  const int tl = (int)threadIdx.x;
   const bool hs = D.clip.has_sat;
   const double satv = D.clip.satv;
   // identical in every thread of the team
@@ -769,8 +777,13 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
           t[NL] += y;  // unclipped over the whole bracket
           t[NL + 1] += X;
         } else if (cnt < lcap) {
-          ly[(size_t)cnt * LS + gt] = y;
-          lX[(size_t)cnt * LS + gt] = X;
+          if (lds_list) {
+            qy[cnt * kBlock + tl] = y;
+            qX[cnt * kBlock + tl] = X;
+          } else {
+            ly[(size_t)cnt * LS + gt] = y;
+            lX[(size_t)cnt * LS + gt] = X;
+          }
           ++cnt;
           t[NL + 3] += 1.0;
         } else {
@@ -815,6 +828,9 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
     PH_T(tl0);
     double t[1] = {0.0};
     int k = 0;
+    if (lds_list) {
+      for (; k < cnt; ++k) t[0] += D.pv(qy[k * kBlock + tl], qX[k * kBlock + tl], lam);
+    }
     for (; k + 4 <= cnt; k += 4) {
       double yv[4], Xv[4];
 #pragma unroll
@@ -887,7 +903,7 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
 // d.g, and the row transforms of d.
 // One image's phase (the kernel below, or the persistent solver's task): the
 // caller has checked st.stop and loaded the twiddles into LDS.
-template <bool COOP, class V>
+template <bool COOP, class V, bool LL = true>
 __device__ __forceinline__ void dir_phase(const SolveArgs& A, int img) {
   BSGP_LDS_VIEWS(A);
   ImgState& st = A.st[img];
@@ -905,8 +921,8 @@ __device__ __forceinline__ void dir_phase(const SolveArgs& A, int img) {
   int evals = 0;
   int64_t ppass = 0, plist_reads = 0;
   if (P.proj_type == 1 && A.plist != nullptr) {
-    ProjOut po = cached_projection(A, img, Pt, tm, D, B, red, st.lam_p, flux, npair, odd, N,
-                                   ppass, plist_reads);
+    ProjOut po = cached_projection<V, LL>(A, img, Pt, tm, D, B, red, lds, st.lam_p, flux, npair,
+                                          odd, N, ppass, plist_reads);
     D.lam_p = po.lam;
     evals = po.evals;
   } else if (P.proj_type == 1) {
@@ -1655,7 +1671,7 @@ __device__ __forceinline__ const SolveArgs& args_of(ArgRef r) {
 }
 template <bool COOP, class V>
 __device__ BSGP_PERSIST_FN void persist_dir(ArgRef r, int img) {
-  dir_phase<COOP, V>(args_of(r), __builtin_amdgcn_readfirstlane(img));
+  dir_phase<COOP, V, false>(args_of(r), __builtin_amdgcn_readfirstlane(img));
 }
 template <bool COOP>
 __device__ BSGP_PERSIST_FN void persist_col_a(ArgRef r, int img) {
