@@ -267,7 +267,7 @@ static int choose_team(const bsgp_plan_s* p, int B, int req) {
 }
 
 static int ensure_team(bsgp_plan p, size_t B, int T) {
-  const size_t np = B * kPartBufs * (size_t)T * kMaxRed;
+  const size_t np = B * kPartBufs * (size_t)(T + 8) * kMaxRed;
   if (T > 1 && np > p->tpart_n) {
     if (p->tpart) HIP_TRY(hipFree(p->tpart));
     p->tpart = nullptr;
@@ -903,9 +903,9 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   // team barrier counters and the timeout word restart at 0 every solve
   HIP_TRY(hipMemsetAsync(p->tctr, 0, p->tctr_bytes, s));
   // flag barriers: every partial slot starts empty
-  if (T > 1 && T <= BSGP_TEAM_FLAGS)
+  if (T > 1 && (T <= BSGP_TEAM_FLAGS || (BSGP_TEAM_HIER && T >= 8)))
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)p->tpart, kPartEmptyWord,
-                              B * kPartBufs * (size_t)T * kMaxRed * 2, s));
+                              B * kPartBufs * (size_t)(T + 8) * kMaxRed * 2, s));
   hipStream_t ss[bsgp_plan_s::kMaxStreams];
   SolveArgs sa[bsgp_plan_s::kMaxStreams];
   if (S > 1) HIP_TRY(hipEventRecord(p->ev_fork, s));

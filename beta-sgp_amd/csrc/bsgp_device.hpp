@@ -32,9 +32,13 @@ constexpr int kMaxRed = 24;  // doubles reduced at once
 // flags (slots pre-filled with kPartEmpty, triple-buffered), so a barrier is
 // one store plus the readers' polls instead of the hierarchical counters'
 // chain of atomics.  Every member polls every member, so larger teams (C4's
-// 256) keep the XCD-hierarchical counters; 0 disables the flags (A/B).
+// 256) go through eight group leaders (BSGP_TEAM_HIER) or keep the
+// XCD-hierarchical counters; 0 disables the flags (A/B).
 #ifndef BSGP_TEAM_FLAGS
 #define BSGP_TEAM_FLAGS 64
+#endif
+#ifndef BSGP_TEAM_HIER
+#define BSGP_TEAM_HIER 1
 #endif
 constexpr int kPartBufs = 3;
 // A signalling NaN (hi word == lo word, so hipMemsetD32 can fill it):
@@ -243,8 +247,8 @@ constexpr int kTeamWords = 17 * kTeamLine;
 
 struct Team {
   int m, T;            // member index, team size
-  double* part;        // [3][T][kMaxRed] partial slots of this image
-  bool flags;          // flag barriers (T <= BSGP_TEAM_FLAGS), else counters
+  double* part;        // [3][T + 8][kMaxRed] partial slots of this image (+ group sums)
+  int flags;           // 1: flag barriers (T <= BSGP_TEAM_FLAGS), 2: via group leaders, 0: counters
   unsigned int* ctr;   // the image's kTeamWords barrier words (monotonic across kernels)
   unsigned int base;   // barriers the team completed before this kernel (same in all members)
   int nb;              // team barriers passed in this kernel
@@ -354,21 +358,33 @@ __device__ __forceinline__ bool part_empty(double v) {
 // those, since every member has arrived at g.  The refill completes before
 // the member's next arrival (both are wave 0's, behind an s_waitcnt), so no
 // member can see a stale partial in a slot it polls.
+//
+// Large teams (flags == 2) go through eight group leaders: group q holds the
+// members m with m % 8 == q and member q leads it.  A leader polls its
+// group's partials (arrival words), folds them and stores the group's sums
+// (word) in row T + q (word T + q); every member polls the eight group rows
+// (words).  Two hops of one store and one poll each instead of T members
+// polling T partials.  The group rows are refilled like the members' rows.
 __device__ __forceinline__ double* team_slot(const Team& t, unsigned int ahead) {
-  return t.part + (size_t)((t.base + (unsigned int)t.nb + ahead) % 3u) * t.T * kMaxRed;
+  return t.part + (size_t)((t.base + (unsigned int)t.nb + ahead) % 3u) * (t.T + 8) * kMaxRed;
 }
 __device__ __forceinline__ void team_refill(const Team& t) {
-  if (threadIdx.x < kMaxRed)
-    __hip_atomic_store((gu64*)(team_slot(t, 2) + (size_t)t.m * kMaxRed + threadIdx.x), kPartEmpty,
+  if (threadIdx.x < kMaxRed) {
+    double* r = team_slot(t, 2);
+    __hip_atomic_store((gu64*)(r + (size_t)t.m * kMaxRed + threadIdx.x), kPartEmpty,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t.flags == 2 && t.m < 8)
+      __hip_atomic_store((gu64*)(r + (size_t)(t.T + t.m) * kMaxRed + threadIdx.x), kPartEmpty,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
-// wave 0: until every member's arrival word is >= n1
-__device__ __forceinline__ void team_wait_words(Team& t, unsigned int n1) {
+// wave 0: until the arrival words w0, w0 + ws, ... (n of them) are >= n1
+__device__ __forceinline__ void team_wait_words(Team& t, int w0, int ws, int n, unsigned int n1) {
   unsigned int spins = 0;
   for (;;) {
     bool ok = true;
-    for (int mm = (int)threadIdx.x; mm < t.T; mm += 64)
-      ok &= (int)(__hip_atomic_load((gu32*)(t.ctr + mm), __ATOMIC_RELAXED,
+    for (int k = (int)threadIdx.x; k < n; k += 64)
+      ok &= (int)(__hip_atomic_load((gu32*)(t.ctr + w0 + k * ws), __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT) - n1) >= 0;
     if (__all(ok)) return;
     if (!team_spin(t, spins)) return;
@@ -392,7 +408,17 @@ __device__ __forceinline__ void team_sync(Team& t) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store((gu32*)(t.ctr + t.m), n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      team_wait_words(t, n1);
+      if (t.flags == 2) {
+        if (t.m < 8) {  // leader: the group's words, then the group's word
+          team_wait_words(t, t.m, 8, (t.T - t.m + 7) >> 3, n1);
+          if (threadIdx.x == 0)
+            __hip_atomic_store((gu32*)(t.ctr + t.T + t.m), n1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        team_wait_words(t, t.T, 1, 8, n1);
+      } else {
+        team_wait_words(t, 0, 1, t.T, n1);
+      }
       if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -431,7 +457,7 @@ __device__ __forceinline__ void team_red_done(Team& t) {
 }
 // This barrier's partial slots.
 __device__ __forceinline__ double* red_slot(const Team& t) {
-  return t.flags ? team_slot(t, 0) : t.part + (size_t)(t.nb & 1) * t.T * kMaxRed;
+  return t.flags ? team_slot(t, 0) : t.part + (size_t)(t.nb & 1) * (t.T + 8) * kMaxRed;
 }
 // Wave 0's poll over the partials: with flag barriers the loads repeat until
 // no partial is empty; otherwise one pass.
@@ -496,11 +522,98 @@ __device__ __forceinline__ void member_partials(const double* v, const double* m
   }
 }
 
+// Wave 0 of a member: poll row `row` of `rows` (when `on`) until none of its
+// NV sums and NM maxima is empty; lanes without a row hold 0 / -inf.
+template <int NV, int NM>
+__device__ __forceinline__ void poll_row(Team& t, const double* rows, int row, bool on,
+                                         double* s, double* m) {
+  unsigned int spins = 0;
+  for (;;) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) s[i] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NM; ++k) m[k] = -INFINITY;
+    if (on) {
+      const double* q = rows + (size_t)row * kMaxRed;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        s[i] = ld_sc1(q + i);
+        ok &= !part_empty(s[i]);
+      }
+#pragma unroll
+      for (int k = 0; k < NM; ++k) {
+        m[k] = ld_sc1(q + NV + k);
+        ok &= !part_empty(m[k]);
+      }
+    }
+    if (red_poll_done(t, ok, spins)) return;
+  }
+}
+
+// NV sums and NM maxima of a large team through its eight group leaders
+// (flags == 2; see team_slot): the member's partials to its row, the leader
+// folds its group (lane k: member q + 8k) into row T + q, every member folds
+// the eight group rows (lane q).  A fixed order, the same in every member.
+template <int NV, int NM>
+__device__ __forceinline__ void team_reduce_hier(double* v, double* mx, double* red, Team& t) {
+  constexpr int NT = NV + NM;
+  static_assert(NT >= 1 && NT <= kMaxRed, "too many values");
+  double* slot = team_slot(t, 0);
+  member_partials<NV, NM>(v, mx, red, slot + (size_t)t.m * kMaxRed);
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    double s[NV + 1], m[NM + 1];
+    if (t.m < 8) {
+      const int q = t.m;
+      poll_row<NV, NM>(t, slot, q + 8 * lane, lane < ((t.T - q + 7) >> 3), s, m);
+      double out = 0.0;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const double r = __shfl(wave_sum(s[i]), 0, 64);
+        if (lane == i) out = r;
+      }
+#pragma unroll
+      for (int k = 0; k < NM; ++k) {
+        const double r = __shfl(wave_max(m[k]), 0, 64);
+        if (lane == NV + k) out = r;
+      }
+      if (lane < NT) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's refills first
+        if (out != out) out = __longlong_as_double(0x7ff8000000000000ll);  // never kPartEmpty
+        st_sc1(slot + (size_t)(t.T + q) * kMaxRed + lane, out);
+      }
+    }
+    poll_row<NV, NM>(t, slot, t.T + lane, lane < 8, s, m);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const double r = wave_sum(s[i]);
+      if (lane == 0) red[kWaves * kMaxRed + i] = r;
+    }
+#pragma unroll
+    for (int k = 0; k < NM; ++k) {
+      const double r = wave_max(m[k]);
+      if (lane == 0) red[kWaves * kMaxRed + NV + k] = r;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = red[kWaves * kMaxRed + i];
+#pragma unroll
+  for (int k = 0; k < NM; ++k) mx[k] = red[kWaves * kMaxRed + NV + k];
+  __syncthreads();
+  team_red_done(t);
+}
+
 // Team sum of NV values: every thread of every member gets the totals.
 template <int NV>
 __device__ __forceinline__ void team_sum(double (&v)[NV], double* red, Team& t) {
   if (t.T == 1) {
     block_sum<NV>(v, red);
+    return;
+  }
+  if (t.flags == 2) {
+    team_reduce_hier<NV, 0>(v, nullptr, red, t);
     return;
   }
   double* slot = red_slot(t);
@@ -555,6 +668,10 @@ __device__ __forceinline__ void team_reduce(double (&v)[NV > 0 ? NV : 1], double
     if constexpr (NV > 0) block_sum<NV>(v, red);
 #pragma unroll
     for (int k = 0; k < NM; ++k) mx[k] = block_max(mx[k], red);
+    return;
+  }
+  if (t.flags == 2) {
+    team_reduce_hier<NV, NM>(v, mx, red, t);
     return;
   }
   double* slot = red_slot(t);
@@ -619,6 +736,11 @@ template <bool MAX>
 __device__ __forceinline__ double team_ext(double v, double* red, Team& t) {
   v = MAX ? block_max(v, red) : block_min(v, red);
   if (t.T == 1) return v;
+  if (t.flags == 2) {  // min as -max(-v): the same value, NaN propagating
+    double m1[1] = {MAX ? v : -v};
+    team_reduce_hier<0, 1>(nullptr, m1, red, t);
+    return MAX ? m1[0] : -m1[0];
+  }
   double* slot = red_slot(t);
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's refills first (flags)

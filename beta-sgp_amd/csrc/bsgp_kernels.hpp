@@ -297,8 +297,8 @@ __device__ __forceinline__ Team make_team(const SolveArgs& A, int img, const Img
   Team t;
   t.T = A.T;
   t.m = A.T == 1 ? 0 : (int)(blockIdx.x % (unsigned)A.T);
-  t.part = A.tpart ? A.tpart + (size_t)img * kPartBufs * A.T * kMaxRed : nullptr;
-  t.flags = A.T > 1 && A.T <= BSGP_TEAM_FLAGS;
+  t.part = A.tpart ? A.tpart + (size_t)img * kPartBufs * (A.T + 8) * kMaxRed : nullptr;
+  t.flags = A.T <= 1 ? 0 : A.T <= BSGP_TEAM_FLAGS ? 1 : (BSGP_TEAM_HIER && A.T >= 8) ? 2 : 0;
   t.ctr = A.tctr ? A.tctr + (size_t)img * kTeamWords : nullptr;
   t.base = (unsigned int)st.bar_base;
   t.nb = 0;
