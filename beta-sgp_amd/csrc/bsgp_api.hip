@@ -858,10 +858,10 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     rc = ensure_plist(p, (size_t)B * a.plist_stride);
     if (rc) return rc;
     a.plist = p->plist;
-    a.list_lds = (BSGP_LIST_LDS && T > 1 &&
-                  (size_t)a.lcap * plan_block(p->g) * 2 * sizeof(double) <= p->lds_fft_bytes)
-                     ? 1
-                     : 0;
+    if (BSGP_LIST_LDS && T > 1) {
+      const size_t fit = p->lds_fft_bytes / ((size_t)plan_block(p->g) * 2 * sizeof(double));
+      a.list_lds = (int)std::min<size_t>((size_t)a.lcap, fit);
+    }
   }
   hipStream_t s = (hipStream_t)stream;
   const int K = (prm->adapt_beta && prm->variant == BSGP_VARIANT_BETA)

@@ -89,7 +89,7 @@ struct SolveArgs {
   double* plist;
   size_t plist_stride;  // doubles per image (both arrays)
   int lcap;             // list capacity per thread (pixels one thread streams)
-  int list_lds;         // teams: the lists live in the transform buffers' LDS
+  int list_lds;         // teams: list entries per thread kept in the transform buffers' LDS
   PwProg pw;            // numpy float32 sum order over N (params.gn_f32)
   int storage;          // BSGP_STORAGE_F64 / F32 (iteration vectors, Bufs<V>)
   size_t spec_off;      // doubles from a slot's start to its spectrum

@@ -708,10 +708,12 @@ constexpr double kProjGuessW = BSGP_PROJ_GUESS_W;
 #define BSGP_PROJ_WIDE_PX 16
 #endif
 
-// Teams whose lists fit the transform buffers (SolveArgs::list_lds: C2, the
-// application's subdivisions) keep them in LDS, which the row pass after the
-// projection is the next to use: an evaluation then reads no global memory
-// (LL: compiled in; the persistent one-workgroup solver keeps global lists).
+// Teams keep the first SolveArgs::list_lds entries of every thread's list in
+// the transform buffers' LDS, which the row pass after the projection is the
+// next to use (C2 and the application's subdivisions: the whole list, so an
+// evaluation reads no global memory; C4: 16 of up to 32 entries), the rest
+// in global memory (LL: compiled in; the persistent one-workgroup solver
+// keeps global lists).
 template <class V, bool LL>
 __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt, Team& tm,
                                      const Dir& D, const Bufs<V>& B, double* red, cd* lds,
@@ -724,9 +726,9 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
   double* ly = A.plist + (size_t)img * A.plist_stride;
   double* lX = ly + A.plist_stride / 2;
   const int lcap = A.lcap;
-  const bool lds_list = LL && A.list_lds != 0;
+  const int nl = LL ? A.list_lds : 0;  // entries per thread in LDS
   double* const qy = reinterpret_cast<double*>(lds);
-  double* const qX = qy + (size_t)lcap * kBlock;
+  double* const qX = qy + (size_t)nl * kBlock;
   const int tl = (int)threadIdx.x;
   const bool hs = D.clip.has_sat;
   const double satv = D.clip.satv;
@@ -777,7 +779,7 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
           t[NL] += y;  // unclipped over the whole bracket
           t[NL + 1] += X;
         } else if (cnt < lcap) {
-          if (lds_list) {
+          if (cnt < nl) {
             qy[cnt * kBlock + tl] = y;
             qX[cnt * kBlock + tl] = X;
           } else {
@@ -828,8 +830,9 @@ __device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt
     PH_T(tl0);
     double t[1] = {0.0};
     int k = 0;
-    if (lds_list) {
-      for (; k < cnt; ++k) t[0] += D.pv(qy[k * kBlock + tl], qX[k * kBlock + tl], lam);
+    if (nl > 0) {
+      const int kl = cnt < nl ? cnt : nl;
+      for (; k < kl; ++k) t[0] += D.pv(qy[k * kBlock + tl], qX[k * kBlock + tl], lam);
     }
     for (; k + 4 <= cnt; k += 4) {
       double yv[4], Xv[4];
