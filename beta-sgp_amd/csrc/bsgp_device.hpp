@@ -1032,11 +1032,8 @@ __device__ __forceinline__ void coop_row_inv_fwd_1(const Geo& G, const Part& D, 
 #ifndef BSGP_COL_TW2
 #define BSGP_COL_TW2 0
 #endif
-__device__ __forceinline__ FftPlan col_plan(const FftPlan& f) {
-  FftPlan c = f;
-  if (!BSGP_COL_TW2) c.lds_tw2 = -1;
-  return c;
-}
+// (a template flag, not a modified copy of the plan: a copy of FftPlan lived
+// in scratch memory and every stage of k_col read its fields from there)
 __device__ __forceinline__ void coop_col_pair_nyq(const Geo& G, cd* spec, const cd* tf, cd* a,
                                                   cd* b) {
   const int t = threadIdx.x;
@@ -1059,7 +1056,7 @@ __device__ __forceinline__ void coop_col_pair_nyq(const Geo& G, cd* spec, const 
     }
   }
   __syncthreads();
-  cd* Z = fft_wide(a, b, col_plan(G.fp), false, t, kBlock, BlockSync());
+  cd* Z = fft_wide<BSGP_COL_TW2>(a, b, G.fp, false, t, kBlock, BlockSync());
   cd* o = (Z == a) ? b : a;
   for (int p = t; p < G.P; p += kBlock) {
     cd A, B;
@@ -1068,7 +1065,7 @@ __device__ __forceinline__ void coop_col_pair_nyq(const Geo& G, cd* spec, const 
     o[p] = cmk(X.x - W.y, X.y + W.x);  // X + i W
   }
   __syncthreads();
-  cd* Y = fft_wide(o, Z, col_plan(G.fp), true, t, kBlock, BlockSync());
+  cd* Y = fft_wide<BSGP_COL_TW2>(o, Z, G.fp, true, t, kBlock, BlockSync());
   for (int p = t; p < G.H; p += kBlock) {
     c0[p] = cmk(Y[p].x, 0.0);
     cN[p] = cmk(Y[p].y, 0.0);
@@ -1105,7 +1102,7 @@ __device__ __forceinline__ void coop_col_conv_1(const Geo& G, const Part& D, cd*
       }
     }
     __syncthreads();
-    cd* Z = fft_wide(a, b, col_plan(G.fp), false, t, kBlock, BlockSync());
+    cd* Z = fft_wide<BSGP_COL_TW2>(a, b, G.fp, false, t, kBlock, BlockSync());
     for (int p0 = 0; p0 < G.P; p0 += kBlock * kCCH) {
       cd tv[kCCH];
 #pragma unroll
@@ -1117,7 +1114,7 @@ __device__ __forceinline__ void coop_col_conv_1(const Geo& G, const Part& D, cd*
       }
     }
     __syncthreads();
-    cd* Y = fft_wide(Z, (Z == a) ? b : a, col_plan(G.fp), true, t, kBlock, BlockSync());
+    cd* Y = fft_wide<BSGP_COL_TW2>(Z, (Z == a) ? b : a, G.fp, true, t, kBlock, BlockSync());
     for (int p = t; p < G.H; p += kBlock) col[p] = Y[p];
     __syncthreads();
   }
@@ -1335,7 +1332,7 @@ __device__ __forceinline__ void coop_col_conv_g(const Geo& G, const Part& D, cd*
     __syncthreads();
     PH_ADD(29, tq0);
     PH_T(tq1);
-    cd* Z = fft_wide(a, b, col_plan(G.fp), false, t, c.nt, BlockSync());
+    cd* Z = fft_wide<BSGP_COL_TW2>(a, b, G.fp, false, t, c.nt, BlockSync());
     if (act) {
       for (int p0 = 0; p0 < G.P; p0 += c.nt * kCCH) {
         cd tv[kCCH];
@@ -1349,7 +1346,7 @@ __device__ __forceinline__ void coop_col_conv_g(const Geo& G, const Part& D, cd*
       }
     }
     __syncthreads();
-    cd* Y = fft_wide(Z, (Z == a) ? b : a, col_plan(G.fp), true, t, c.nt, BlockSync());
+    cd* Y = fft_wide<BSGP_COL_TW2>(Z, (Z == a) ? b : a, G.fp, true, t, c.nt, BlockSync());
     if (act)
       for (int p = t; p < G.H; p += c.nt) col[p] = Y[p];
     __syncthreads();

@@ -460,11 +460,19 @@ extern __shared__ __attribute__((aligned(16))) char bsgp_dyn_lds[];
 
 // Workgroup-wide transform (all kBlock-style lanes, `sync` = workgroup
 // barrier): compile-time radix-8 plan for 2048 (config C4), runtime plan otherwise.
-template <class Sync>
+#ifndef BSGP_COOP_TW2
+#define BSGP_COOP_TW2 1
+#endif
+// TW2 false: the global table even where the plan placed the LDS two-level
+// table (the column kernel's register budget, bsgp_device.hpp col_tw2).
+template <bool TW2 = true, class Sync>
 BSGP_HD cd* fft_wide(cd* a, cd* b, const FftPlan& p, bool inv, int lane, int nlanes, Sync sync) {
   if (p.n == 2048) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    if (p.lds_tw2 >= 0) {  // the two-level table in LDS (bsgp_plan_create, load_tw_lds)
+    // the two-level table in LDS (bsgp_plan_create places it for every
+    // 2048-point plan when BSGP_COOP_TW2; load_tw_lds): a compile-time choice,
+    // so the kernels carry one 2048-point transform, not both
+    if constexpr (TW2 && BSGP_COOP_TW2) {
       const cd* t = reinterpret_cast<const cd*>(bsgp_dyn_lds + p.lds_tw2);
       return fft_run_static<2048, true, true>(a, b, Tw2{t, t + 64}, inv, lane, nlanes, sync);
     }

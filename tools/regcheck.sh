@@ -2,7 +2,7 @@
 # Print VGPR / spill / scratch of every kernel in a solver translation unit
 # (gfx950).  Usage: tools/regcheck.sh [file.hip (default bsgp_solver.hip)] [extra hipcc flags]
 set -e
-R=$(cd "$(dirname "$0")/.." && pwd)
+R=${REGROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 SRC=${1:-bsgp_solver.hip}; shift || true
 D=$(mktemp -d)
 cd $D
