@@ -715,7 +715,7 @@ constexpr double kProjGuessW = BSGP_PROJ_GUESS_W;
 // in global memory (LL: compiled in; the persistent one-workgroup solver
 // keeps global lists).
 template <class V, bool LL>
-__device__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt, Team& tm,
+__device__ __forceinline__ ProjOut cached_projection(const SolveArgs& A, int img, const Part& Pt, Team& tm,
                                      const Dir& D, const Bufs<V>& B, double* red, cd* lds,
                                      double lam_prev, double flux, int npair, bool odd, int N,
                                      int64_t& passes, int64_t& list_reads) {
