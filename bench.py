@@ -589,7 +589,11 @@ def main():
         def sync():
             pass
     else:
-        torch.cuda.set_device(local)
+        # BSGP_RANK_DEVICE: every rank on this one device (the multi-rank path
+        # rehearsed on a one-GPU box, tests/test_gpu_multirank.py); set before
+        # any GPU call of the rank
+        dev_override = os.environ.get("BSGP_RANK_DEVICE")
+        torch.cuda.set_device(int(dev_override) if dev_override is not None else local)
         import _bsgp
         import sgp
         if stamps:
@@ -679,6 +683,7 @@ def main():
         "config": {"workload": workload, "images_per_gpu": B,
                    "images_total": cfg.get("total", B * world), "image": [n, n], "psf": [k, k],
                    "maxit": args.maxit,
+                   "iterations_per_step": tot,
                    "parallelism": f"{world} independent shards, one process per GPU "
                                   f"(no collective on the data path)"},
         "roofline": None,
@@ -686,6 +691,9 @@ def main():
     }
     if args.config in PUBLISHED_CONTEXT:
         result["context"] = PUBLISHED_CONTEXT[args.config]
+    if os.environ.get("BSGP_RANK_DEVICE") is not None and not args.stub:
+        result["config"]["parallelism"] += (f"; every rank on device {os.environ['BSGP_RANK_DEVICE']}"
+                                            " (BSGP_RANK_DEVICE rehearsal, not a scaling figure)")
     if args.stub:
         result["data"] = "stub: harness test without a GPU"
         print(json.dumps(result), flush=True)

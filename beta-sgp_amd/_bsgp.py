@@ -170,7 +170,8 @@ class Plan:
     _leased = False  # held by a solve (lease_plan)
     _done = None  # event after the last leased solve's launches
 
-    def __init__(self, H, W, psf, conv_mode, device=None, storage=BSGP_STORAGE_F64):
+    def __init__(self, H, W, psf, conv_mode, device=None, storage=BSGP_STORAGE_F64,
+                 psf_checked=False):
         require_gpu()
         if device is None:
             device = torch.cuda.current_device()
@@ -181,11 +182,13 @@ class Plan:
         self.device = device
         self.storage = storage
         h = ctypes.c_void_p()
-        # the drop-in checks the PSF's normalisation itself, in the caller's
-        # dtype (sgp._check_psf, check_psf_once; per-image PSFs in
-        # bsgp_plan_set_psfs), so the library's float64 check is skipped
+        # psf_checked: the caller has checked the PSF's normalisation itself,
+        # in its own dtype (the drop-in's pool and per-image plans, after
+        # sgp._check_psf / check_psf_once), so the library's float64 check is
+        # skipped; a direct construction keeps the library's check
         rc = lib().bsgp_plan_create_checked(self.H, self.W, psf.ctypes.data, self.kh, self.kw,
-                                            conv_mode, storage, device, 1, ctypes.byref(h))
+                                            conv_mode, storage, device, int(bool(psf_checked)),
+                                            ctypes.byref(h))
         if rc != 0:
             raise BsgpError(rc, lib().bsgp_last_error().decode(errors="replace"))
         self.h = h
@@ -353,7 +356,7 @@ def _plan_key(H, W, psf, conv_mode, storage):
 
 
 def _new_plan(H, W, psf, key):
-    p = Plan(H, W, psf, key[4], key[6], storage=key[5])
+    p = Plan(H, W, psf, key[4], key[6], storage=key[5], psf_checked=True)
     p._psf_host = psf.copy()  # (the caller may rewrite its array later)
     return p
 
@@ -457,7 +460,8 @@ def per_image_plan(H, W, psfs, conv_mode, storage="f64"):
     # the plan-building kernels read them there
     dev = (psfs.to(device=torch.cuda.current_device(), dtype=torch.float64).contiguous()
            if torch.is_tensor(psfs) else to_dev(psfs))
-    p = Plan(H, W, dev[0].cpu().numpy(), conv_mode, storage=storage_code(storage))
+    p = Plan(H, W, dev[0].cpu().numpy(), conv_mode, storage=storage_code(storage),
+             psf_checked=True)
     return p.set_psfs(dev)
 
 

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cstdlib>
 #include <cmath>
@@ -176,7 +177,7 @@ struct bsgp_plan_s {
   int* active_h = nullptr;   // pinned host mirror for polling
   int* done_h = nullptr;     // host-mapped: the solve seq once every image has stopped
   int* done_d = nullptr;     // (its device address)
-  int seq = 0;               // solves started on this plan
+  int seq = 0;               // the last solve's sequence number (process-wide counter)
   static constexpr int kPollRing = 8;
   hipEvent_t ev_it[kPollRing] = {};  // after iteration it on stream 0 (lookahead polling)
   // sub-batch streams: phases of different sub-batches overlap on the device
@@ -251,6 +252,11 @@ static int ensure_ws(bsgp_plan p, size_t slots) {
 // CU the runtime reports for every team kernel of the plan's build
 // (p->resident_per_cu, hipOccupancyMaxActiveBlocksPerMultiprocessor).  Each
 // member keeps at least one row pair and one column per FFT wave.
+// Solve sequence numbers for the lookahead poll's host-mapped word: one
+// process-wide counter, so no plan (nor a reused pinned block) ever sees a
+// value another solve wrote.
+static std::atomic<int> g_solve_seq{0};
+
 static int choose_team(const bsgp_plan_s* p, int B, int req) {
   if (req == 1) return 1;
   const Geo& g = p->g;
@@ -263,6 +269,9 @@ static int choose_team(const bsgp_plan_s* p, int B, int req) {
   int T = std::min(p->ncu / B, tgeo);
   if (req > 1) T = std::min(req, tgeo);
   T = std::min(T, res);
+  // the barrier words and the group leaders' polls cover at most kMaxTeam
+  // members (bsgp_device.hpp)
+  T = std::min(T, kMaxTeam);
   return T < 1 ? 1 : T;
 }
 
@@ -624,6 +633,9 @@ int bsgp_plan_create_checked(int32_t H, int32_t W, const double* psf, int32_t kh
     bsgp_plan_destroy(p);
     return fail(BSGP_ERR_HIP, "counter allocation failed");
   }
+  // a reused pinned block may still hold an old plan's seq; seqs
+  // also come from one process-wide counter, so a stale word never matches
+  *p->done_h = 0;
   *out = p;
   return BSGP_OK;
 }
@@ -883,6 +895,12 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   // so it runs the whole batch as one sub-batch
   const bool persist = prm->persistent && T == 1 && (!p->g.coop || BSGP_COOP512) && !track;
   if (persist) S = 1;
+  // fixed-length persistent solves run every image's setup as the first task
+  // of its chain inside k_persist: the setups of the last images overlap the
+  // first iterations of the others, with no k_setup launch and no boundary
+  // (BSGP_FOLD_SETUP=0: k_setup first, for A/B)
+  const bool ring = prm->stop_criterion >= 2 && prm->stop_criterion <= 4;
+  a.fold_setup = (persist && !ring && env_knob("BSGP_FOLD_SETUP", 1, 0, 1)) ? 1 : 0;
   // sub-batch 0 runs on the caller's stream itself, sub-batches 1..S-1 on the
   // plan's streams: S streams in all, so S = 4 fits the 4 hardware queues HIP
   // opens per process (GPU_MAX_HW_QUEUES)
@@ -898,7 +916,8 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
   // the setup or k_bb stops (count_stopped); the last one writes this solve's
   // seq to the host-mapped word
   HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)p->active, B, 1, s));
-  a.seq = ++p->seq;
+  a.seq = g_solve_seq.fetch_add(1, std::memory_order_relaxed) + 1;
+  p->seq = a.seq;
   a.done_host = p->done_d;
   // team barrier counters and the timeout word restart at 0 every solve
   HIP_TRY(hipMemsetAsync(p->tctr, 0, p->tctr_bytes, s));
@@ -916,7 +935,7 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
     sa[j].img0 = (int)((int64_t)B * j / S);
     sa[j].nimg = (int)((int64_t)B * (j + 1) / S) - sa[j].img0;
     if (prof) HIP_TRY(hipEventRecord(prof->ev[0], ss[j]));
-    HIP_TRY(launch_setup(sa[j], p->lds_bytes, ss[j]));
+    if (!a.fold_setup) HIP_TRY(launch_setup(sa[j], p->lds_bytes, ss[j]));
     if (prof) HIP_TRY(hipEventRecord(prof->ev[1], ss[j]));
     if (track) HIP_TRY(launch_track(sa[j], 0, ss[j]));
   }

@@ -244,6 +244,12 @@ typedef __attribute__((address_space(1))) int gi32;
 // generation word, and one top counter of completed groups.
 constexpr int kTeamLine = 32;
 constexpr int kTeamWords = 17 * kTeamLine;
+// Largest team: flag barriers use words ctr[m] (m < T) and, through the
+// group leaders, ctr[T + q] (q < 8); a leader polls its group with one row
+// per lane of wave 0 (members q + 8 * lane).  choose_team clamps T to this.
+constexpr int kMaxTeam = 512;
+static_assert(kMaxTeam + 8 <= kTeamWords, "team barrier words overflow the image's block");
+static_assert(kMaxTeam <= 8 * 64, "a group leader polls at most 64 members");
 
 struct Team {
   int m, T;            // member index, team size

@@ -97,6 +97,8 @@ struct SolveArgs {
                         // (sgp.py:336) by trial ceil(log 1e-12 / log beta) + 1 for 0 < beta < 1
   unsigned spin_limit;  // persistent solver: s_sleep polls before a hand-off wait gives up
                         // (status bit 4); 2^26 unless BSGP_SPIN_LIMIT says otherwise (tests)
+  int fold_setup;       // persistent solver, slot order: every image's setup is the first
+                        // task of its chain inside k_persist (no k_setup launch)
 };
 
 hipError_t launch_setup(const SolveArgs& a, size_t lds, hipStream_t s);

@@ -334,7 +334,7 @@ __device__ __forceinline__ bool leader(const Team& t) { return t.m == 0 && threa
 // level by level with a team barrier between levels, then the chunk fold
 // res = res + root from 0.  `vals` is float scratch in HBM (leaves + nodes).
 template <class TERM>
-__device__ float np_f32_sum(const PwProg& pw, TERM&& term, float* vals, const Part& D, Team& tm) {
+__device__ __forceinline__ float np_f32_sum(const PwProg& pw, TERM&& term, float* vals, const Part& D, Team& tm) {
   const int* lv = pw.prog;
   const int* nd = lv + 2 * pw.nleaf;
   const int* off = nd + 2 * pw.nnode;
@@ -417,10 +417,22 @@ __device__ __forceinline__ void count_stopped(const SolveArgs& A) {
 // ------------------------------------------------------------ kernel: setup
 // sgp.py:163-298 (= 617-742): scaling, null pixels, flux, x0, initial
 // projection, x_tf = A(x), f, g and the scaling-matrix bounds.
+// Waves per SIMD the setup kernel is compiled for (per-wave plans; 0: the
+// compiler's choice).  Setup runs once per solve, one workgroup per image:
+// at four workgroups per CU C3's 1024 images are one round instead of two.
+#ifndef BSGP_SETUP_WAVES
+#define BSGP_SETUP_WAVES 0
+#endif
+#if BSGP_SETUP_WAVES
+#define BSGP_SETUP_ATTR __attribute__((amdgpu_waves_per_eu(COOP ? 1 : BSGP_SETUP_WAVES)))
+#else
+#define BSGP_SETUP_ATTR
+#endif
+// One image's setup (k_setup below, or the persistent solver's first task of
+// the image, SolveArgs::fold_setup); the caller has loaded the twiddles into LDS.
 template <bool COOP, class V>
-__global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
+__device__ __forceinline__ void setup_phase(const SolveArgs& A, int img) {
   BSGP_LDS_VIEWS(A);
-  const int img = team_img(A);
   const Geo& G = A.g;
   const bsgp_params& P = A.prm;
   const int N = G.H * G.W;
@@ -433,7 +445,6 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
   Team tm = make_team(A, img, st);
   tm.base = 0;
   const Part D = make_part(tm, G.nfw, G.W);
-  load_tw_lds(G);
   const double* gn_in = A.in.gn + (size_t)img * N;
   const double* bk_in = bmap ? A.in.bkg + (size_t)img * N : nullptr;
   const double bk_scalar_raw = bmap ? 0.0 : A.in.bkg[img];
@@ -672,6 +683,12 @@ __global__ void __launch_bounds__(kBlock) k_setup(SolveArgs A) {
       count_stopped(A);
     }
   }
+}
+
+template <bool COOP, class V>
+__global__ void __launch_bounds__(kBlock) BSGP_SETUP_ATTR k_setup(SolveArgs A) {
+  load_tw_lds(A.g);
+  setup_phase<COOP, V>(A, team_img(A));
 }
 
 // --------------------------------------- projection with pixel lists
@@ -1673,6 +1690,10 @@ __device__ __forceinline__ const SolveArgs& args_of(ArgRef r) {
   return *(const SolveArgs*)p;
 }
 template <bool COOP, class V>
+__device__ BSGP_PERSIST_FN void persist_setup(ArgRef r, int img) {
+  setup_phase<COOP, V>(args_of(r), __builtin_amdgcn_readfirstlane(img));
+}
+template <bool COOP, class V>
 __device__ BSGP_PERSIST_FN void persist_dir(ArgRef r, int img) {
   dir_phase<COOP, V, false>(args_of(r), __builtin_amdgcn_readfirstlane(img));
 }
@@ -1723,7 +1744,11 @@ __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs 
   const Geo& G = A.g;
   load_tw_lds(G);
   const unsigned nimg = (unsigned)A.nimg;
-  const unsigned total = (unsigned)A.prm.MAXIT * nimg;
+  // fold_setup (slot order only): task t = kk * nimg + i is image i's kk-th
+  // task, the setup first (kk = 0), then iteration kk; without it iteration
+  // kk + 1.  Either way task kk waits for done[i] >= kk and publishes kk + 1.
+  const unsigned fs = A.fold_setup ? 1u : 0u;
+  const unsigned total = ((unsigned)A.prm.MAXIT + fs) * nimg;
   const bool use_ring = A.prm.stop_criterion >= 2 && A.prm.stop_criterion <= 4;
   unsigned long long* ring = reinterpret_cast<unsigned long long*>(queue + 4);
   for (;;) {
@@ -1754,7 +1779,8 @@ __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs 
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           // stopped by the setup (status 8) before its first iteration: it
-          // leaves the ring (the setup did not count it as running)
+          // leaves the ring (the setup already counted it down from B in
+          // count_stopped, so it is not among the running images)
           if (A.st[img].stop) img = -2;
         }
       } else {
@@ -1764,7 +1790,7 @@ __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs 
           t = total;  // every image has stopped: nothing left to run
         if (t < total) {
           img = A.img0 + (int)(t % nimg);
-          const unsigned need = t / nimg;  // iterations of img that must be done
+          const unsigned need = t / nimg;  // tasks of img that must be done
           k = need + 1;
           unsigned d = ld_sc1_u32(done + img), spins = 0;
           while (d < need) {
@@ -1784,7 +1810,8 @@ __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs 
             } else {
               __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
               asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-              if (need == 0 && A.st[img].stop) {
+              // (a folded setup publishes its own stop, below)
+              if (!fs && need == 0 && A.st[img].stop) {
                 // stopped by the setup (status 8): published as stopped
                 __hip_atomic_store((gu32*)(done + img), kDoneStop, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -1805,18 +1832,22 @@ __global__ void __launch_bounds__(kBlock) BSGP_PERSIST_ATTR k_persist(SolveArgs 
     if (img == -1) break;
     if (img < 0) continue;
     const ArgRef ar = kernarg_ref();
-    persist_dir<COOP, V>(ar, img);
-    __syncthreads();  // rows of d and the direction scalars complete
-    persist_col_a<COOP>(ar, img);
-    persist_ls<K, MODE, ADAPT, COOP, V, SB>(ar, img);
-    __syncthreads();  // the accepted step and AT's columns complete
-    persist_bb<COOP, V>(ar, img);
+    if (fs && k == 1) {
+      persist_setup<COOP, V>(ar, img);  // the image's first task: its setup
+    } else {
+      persist_dir<COOP, V>(ar, img);
+      __syncthreads();  // rows of d and the direction scalars complete
+      persist_col_a<COOP>(ar, img);
+      persist_ls<K, MODE, ADAPT, COOP, V, SB>(ar, img);
+      __syncthreads();  // the accepted step and AT's columns complete
+      persist_bb<COOP, V>(ar, img);
+    }
     // hand the image on: every wave's stores drained, then lane 0 releases at
     // agent scope and publishes (sc1 store): ring append, or done[img]
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      const bool stopped = A.st[img].stop != 0;  // lane 0 is bb's leader: its own write
+      const bool stopped = A.st[img].stop != 0;  // lane 0 is bb's (setup's) leader: its own write
       if (use_ring) {
         if (!stopped) {
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Interleaved A/B/... benchmark, REPS rounds, median per variant.
 # Usage: bash scripts/gpu_ab.sh TAG REPS spec... [-- common bench args]
-#   spec = LIB[,extra,bench,args]   LIB "base" = libbsgp.so, else libbsgp_LIB.so
+#   spec = LIB[,extra,bench,args][,NAME=VALUE env]   LIB "base" = libbsgp.so, else libbsgp_LIB.so
 set -o pipefail
 TAG=$1; REPS=$2; shift 2
 SPECS=()
@@ -11,9 +11,12 @@ cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
 for ((i=0; i<REPS; i++)); do
   for k in "${!SPECS[@]}"; do
     IFS=',' read -ra PARTS <<< "${SPECS[$k]}"
-    V=${PARTS[0]}; EXTRA=("${PARTS[@]:1}")
+    V=${PARTS[0]}; EXTRA=(); ENVS=()
+    for x in "${PARTS[@]:1}"; do
+      if [[ "$x" == --* || "$x" != *=* ]]; then EXTRA+=("$x"); else ENVS+=("$x"); fi
+    done
     L=$PWD/beta-sgp_amd/libbsgp_$V.so; [ "$V" == "base" ] && L=$PWD/beta-sgp_amd/libbsgp.so
-    BSGP_LIB=$L timeout -k 10 300 python bench.py --no-cpu --steps 3 "${EXTRA[@]}" "$@" > gpurun_out/${TAG}_${k}_$i.json 2> gpurun_out/${TAG}_${k}_$i.err || { echo "bench ${SPECS[$k]} failed"; tail -3 gpurun_out/${TAG}_${k}_$i.err; exit 3; }
+    env "${ENVS[@]}" BSGP_LIB=$L timeout -k 10 300 python bench.py --no-cpu --steps 3 "${EXTRA[@]}" "$@" > gpurun_out/${TAG}_${k}_$i.json 2> gpurun_out/${TAG}_${k}_$i.err || { echo "bench ${SPECS[$k]} failed"; tail -3 gpurun_out/${TAG}_${k}_$i.err; exit 3; }
   done
 done
 python - "$TAG" "$REPS" "${SPECS[@]}" <<'PY'

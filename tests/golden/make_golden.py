@@ -5,6 +5,7 @@ exist on the GPU box).  The committed .npz files are data (inputs + expected
 outputs); this script is how they were made:
 
     cd /root/repo && PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py circular
+    cd /root/repo && PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py sampling
     cd /root/repo && PYTHONDONTWRITEBYTECODE=1 /opt/conda/bin/python3.9 tests/golden/make_golden.py linear
     cd /root/repo && PYTHONDONTWRITEBYTECODE=1 /opt/conda/bin/python3.9 tests/golden/make_golden.py app
     cd /root/repo && NPY_DISABLE_CPU_FEATURES="$LIBM_FEATURES" PYTHONDONTWRITEBYTECODE=1 \
@@ -867,6 +868,52 @@ def make_crowded():
         print(f"{name:14s} {fn:12s} iters={it:3d} discr0={discr[0]:.10f} discrN={discr[-1]:.10f}")
 
 
+def make_sampling():
+    """simulation_test_sgp.py:57-110 with do_sampling=True on NGC7027 (py3.10 /
+    numpy 2.2, circular A): 30 initial betas from np.random.seed(42) and
+    np.random.normal(loc=1, scale=0.05) (:68-73), each an adaptive-beta
+    sgp_betaDiv run (init_recon 3, stop rule 1, MAXIT 27, lr 1e-3,
+    lr_exp_param 0.1, schedule_lr, :77-81) scored by rel_err against obj
+    (:83-85), the strict running minimum (:92-94), then the final run with the
+    chosen beta and adapt_beta=False (:100-108).  The search loop is restated
+    here (the reference's function also plots and uses np.Inf, which numpy 2
+    removed); every solve is the reference's own sgp_betaDiv.  Stored: the
+    candidates' betas, rel_err, iterations and discrepancies, the chosen beta,
+    the best candidate's x, the final run's x, discr and rel_err."""
+    from scipy.io import loadmat
+    sgp, fcp = import_reference(need_astropy=False)
+    ngc = loadmat(os.path.join(REF, "simulated_test/data/NGC7027_255.mat"))
+    image, psf, bkg, obj = ngc["gn"], ngc["psf"], ngc["bg"][0][0], ngc["obj"]
+
+    def relerr(x):
+        e = x - obj
+        return float(np.sqrt(np.sum(e * e) / np.sum(obj * obj)))
+
+    np.random.seed(42)
+    rands = [np.random.normal(loc=1, scale=0.05) for _ in range(30)]
+    kw = dict(init_recon=3, stop_criterion=1, MAXIT=27, lr=1e-3, lr_exp_param=0.1,
+              schedule_lr=True)
+    errs, its, discrs, best, best_err, best_x = [], [], [], None, np.inf, None
+    for b in rands:
+        x, it, discr, _, _ = run_quiet(sgp.sgp_betaDiv, image, psf, bkg, betaParam=b,
+                                       adapt_beta=True, **kw)
+        e = relerr(x)
+        errs.append(e)
+        its.append(it)
+        discrs.append(discr)
+        if e < best_err:
+            best_err, best, best_x = e, b, x
+        print(f"beta-init {b:.16f} rel_err {e:.12f} iters {it}")
+    xf, itf, discrf, _, _ = run_quiet(sgp.sgp_betaDiv, image, psf, bkg, betaParam=best,
+                                      adapt_beta=False, **kw)
+    np.savez_compressed(os.path.join(OUT, "ref_ngc_sampling.npz"), betas=np.array(rands),
+                        relerr=np.array(errs), iters=np.array(its), discr=np.array(discrs),
+                        best_beta=np.array(best), best_relerr=np.array(best_err), best_x=best_x,
+                        final_x=xf, final_iters=np.array(itf), final_discr=discrf,
+                        final_relerr=np.array(relerr(xf)), kwargs=repr(kw))
+    print(f"best beta-init {best!r} rel_err {best_err:.12f}; final run rel_err {relerr(xf):.12f}")
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "circular"
     cwd = os.getcwd()
@@ -895,6 +942,8 @@ if __name__ == "__main__":
                 make_stamps()
             elif which == "crowded":
                 make_crowded()
+            elif which == "sampling":
+                make_sampling()
             elif which == "satellite":
                 make_satellite()
             else:

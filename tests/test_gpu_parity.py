@@ -181,6 +181,41 @@ def test_solve_matches_reference_ngc(name, sgpmod, ngc, capsys):
     np.testing.assert_allclose(discr, fx["discr"], rtol=1e-7)
 
 
+def test_ngc_do_sampling_search_one_launch(sgpmod, ngc):
+    """simulation_test_sgp.py:57-110 with do_sampling=True: the reference's 30
+    adaptive-beta candidates (np.random.seed(42), normal(1, 0.05), MAXIT 27)
+    as ONE batched launch through sgp_betaDiv_multistart with the test's own
+    score, rel_err against the ground truth (:83-85): every candidate's rel_err
+    and discrepancy against the unchanged reference's run, the reference's
+    choice by its strict running minimum (:92-94), then the final fixed-beta
+    run with that beta (:100-108) against the reference's x and rel_err."""
+    gn, psf, bkg, obj = ngc
+    fx = golden("ref_ngc_sampling.npz")
+    kw = dict(init_recon=3, stop_criterion=1, MAXIT=27, lr=1e-3, lr_exp_param=0.1,
+              schedule_lr=True)
+
+    def relerr(x):
+        e = x - obj
+        return float(np.sqrt(np.sum(e * e) / np.sum(obj * obj)))
+
+    betas = [float(b) for b in fx["betas"]]
+    _, info = sgpmod.sgp_betaDiv_multistart(gn, psf, bkg, betas=betas, score=relerr,
+                                            final_solve=False, adapt_beta=True, **kw)
+    assert len(info["candidates"]) == 30
+    for i, (x, it, discr, _, _) in enumerate(info["candidates"]):
+        assert it == int(fx["iters"][i])
+        assert abs(info["scores"][i] / fx["relerr"][i] - 1) < 1e-7, (i, info["scores"][i])
+        np.testing.assert_allclose(discr, fx["discr"][i], rtol=1e-7)
+    # the reference's pick (a 5.5e-3 relative gap to the runner-up)
+    assert info["best_beta"] == float(fx["best_beta"])
+    assert rel(info["candidates"][info["best"]][0], fx["best_x"]) < SOLVE_RTOL
+    x, it, discr, _, _ = sgpmod.sgp_betaDiv(gn, psf, bkg, betaParam=info["best_beta"],
+                                            adapt_beta=False, **kw)
+    assert it == int(fx["final_iters"]) and rel(x, fx["final_x"]) < SOLVE_RTOL
+    assert abs(relerr(x) / float(fx["final_relerr"]) - 1) < 1e-7
+    np.testing.assert_allclose(discr, fx["final_discr"], rtol=1e-7)
+
+
 def test_ngc_kl27_known_answer(sgpmod, ngc):
     """simulation_test_sgp.py:17-34: rel. error vs ground truth 0.137887788241."""
     gn, psf, bkg, obj = ngc

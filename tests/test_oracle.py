@@ -33,6 +33,35 @@ def test_oracle_ngc_kl27_relerr(ngc):
     assert len(discr) == 28 and abs(discr[0] - 40.825519776418) < 1e-9
 
 
+def test_oracle_ngc_do_sampling_candidates(ngc):
+    """simulation_test_sgp.py:65-96 (do_sampling=True on NGC7027): the
+    reference's 30 initial betas (np.random.seed(42), normal(1, 0.05)) are
+    reproduced exactly; three of its adaptive-beta candidates (the chosen one,
+    the runner-up and the worst) give the reference's rel_err, and the final
+    fixed-beta run (:100-108) its x.  The whole 30-candidate search is the GPU
+    test (test_gpu_parity.test_ngc_do_sampling_search_one_launch)."""
+    gn, psf, bkg, obj = ngc
+    fx = golden("ref_ngc_sampling.npz")
+    np.random.seed(42)
+    rands = [np.random.normal(loc=1, scale=0.05) for _ in range(30)]
+    np.testing.assert_array_equal(rands, fx["betas"])
+    kw = dict(init_recon=3, stop_criterion=1, MAXIT=27, lr=1e-3, lr_exp_param=0.1,
+              schedule_lr=True)
+    err = fx["relerr"]
+    order = np.argsort(err)
+    for i in (order[0], order[1], order[-1]):
+        x, it, discr, _, _ = orc.sgp_betaDiv(gn, psf, bkg, betaParam=fx["betas"][i],
+                                             adapt_beta=True, **kw)
+        r = np.sqrt(np.sum((x - obj) ** 2) / np.sum(obj * obj))
+        assert it == int(fx["iters"][i])
+        assert abs(r / err[i] - 1) < 1e-9, (i, r, err[i])
+        np.testing.assert_allclose(discr, fx["discr"][i], rtol=1e-9)
+    assert fx["best_beta"] == fx["betas"][order[0]]
+    x, it, _, _, _ = orc.sgp_betaDiv(gn, psf, bkg, betaParam=float(fx["best_beta"]),
+                                     adapt_beta=False, **kw)
+    assert np.linalg.norm(x - fx["final_x"]) / np.linalg.norm(fx["final_x"]) < 1e-9
+
+
 def test_oracle_stamp31_odd_fftshift():
     fx = golden("ref_stamp31_beta_adapt.npz")
     x, it, discr, _, _ = orc.sgp_betaDiv(fx["gn"], fx["psf"], np.float64(20.0), init_recon=2,
