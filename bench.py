@@ -479,6 +479,14 @@ def kernel_bytes(H, W, P, Qh, counters, iters, beta, series, compact, bmap, fuse
                  + (it * col_per if fused_at_col else 0.0))
     b["k_bb"] = it * (S + N * ((vb if beta else 0.0) + 2.0 * vb) + 2.0 * vb * N)
     b["k_col"] = it * col_per * (1.0 if fused_at_col else 2.0)
+    # setup (once per image, k_setup or the persistent solver's first task):
+    # raw statistics 8, scale 8+8, null fill + start x 8+8+8, the start's
+    # projection with one evaluation and the clip (a lower bound: the setup's
+    # evaluations are not counted on the device) 8+8+8, rows of x 8, rows of
+    # A(x) with f, pw 8+8+8, rows of AT(w) pw + g 8+8, rows of gn 8, compact
+    # gn 8+4 = 140 B/px; spectra: 7 row passes + three column passes 3(2S+TF)
+    nimg = float(counters.shape[0])
+    b["k_setup"] = nimg * (140.0 * N + 12.0 * S + 3.0 * TF)
     return b
 
 
@@ -771,9 +779,11 @@ def profile_kernels(kw, gn, psf, bkg, n):
                       series=not kl and not kw.get("adapt_beta", False),
                       compact=sgp.GN_COMPACT_DEFAULT == 1, bmap=False,
                       fused_at_col=(team == 1), vb=4.0 if kw["storage"] == "f32" else 8.0)
-    kb["k_persist"] = float(sum(kb.values()))
-    names = ["k_setup", "k_dir", "k_col", "k_ls", "k_bb", "k_persist"]
     ms, nl = prof["kernel_ms"], prof["launches"]
+    # the persistent launch holds every iteration, and the setups too when
+    # they are folded into it (no k_setup launch, SolveArgs::fold_setup)
+    kb["k_persist"] = float(sum(v for k, v in kb.items() if k != "k_setup" or nl[0] == 0))
+    names = ["k_setup", "k_dir", "k_col", "k_ls", "k_bb", "k_persist"]
     kernels = {}
     for i, name in enumerate(names):
         if i == 0 or nl[i] == 0:
@@ -785,7 +795,7 @@ def profile_kernels(kw, gn, psf, bkg, n):
         kernels[name] = {"ms_total": float(ms[i]), "launches": int(nl[i]),
                          "ms_per_launch": float(per_ms), "bytes_per_launch": float(per_b),
                          "achieved": float(ach), "frac": float(ach / HBM_PEAK_GBS)}
-    alg_total = float(sum(v for k, v in kb.items() if k != "k_persist"))
+    alg_total = float(sum(v for k, v in kb.items() if k != "k_persist"))  # (setup included)
     return kernels, alg_total, cnt, iters, float(np.sum(ms))
 
 
@@ -803,8 +813,10 @@ def roofline(args, kw, gn, psf, bkg, B, n, solve_ms):
         tr_src = (f"profiles/traffic_{args.config}.json (committed PMC record, not this run): "
                   + str(traffic.get("note", "")))
     if dom == "k_persist":
+        folded = kernels["k_setup"]["launches"] == 0
         unit = (f"one launch = the whole solve: {B} images x {int(iters.max())} iterations, "
-                f"every phase (persistent task-queue kernel)")
+                f"every phase (persistent task-queue kernel)"
+                + (", and every image's setup as its first task" if folded else ""))
     else:
         unit = f"one launch = {B} images x one iteration of {dom} (profiled solve on one stream)"
     out = {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS,

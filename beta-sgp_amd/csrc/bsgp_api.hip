@@ -966,8 +966,9 @@ static int solve_impl(bsgp_plan p, int32_t B, const bsgp_params* prm, const bsgp
       }
       float ms = 0.f;
       HIP_TRY(hipEventElapsedTime(&ms, prof->ev[0], prof->ev[1]));
-      prof->kernel_ms[0] = ms;
-      prof->launches[0] = 1;
+      // (a folded setup runs inside k_persist: no k_setup launch)
+      prof->kernel_ms[0] = a.fold_setup ? 0.0 : ms;
+      prof->launches[0] = a.fold_setup ? 0 : 1;
       HIP_TRY(hipEventElapsedTime(&ms, prof->ev[2], prof->ev[3]));
       prof->kernel_ms[5] = ms;
       prof->launches[5] = 1;

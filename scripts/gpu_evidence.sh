@@ -1,6 +1,7 @@
 #!/bin/bash
 # Evidence from ONE lease: smoke, PMC traffic (two passes) copied to
-# profiles/traffic_c3.json, the default bench line (C3) that reads it, the
+# profiles/traffic_c3.json, the driver's bench command (C3: --gpus 1 --steps 20
+# --warmup 5) that reads it, the
 # rocprofv3 kernel statistics of the same command, SQ counters of k_persist,
 # and the other configuration lines.  Usage: bash scripts/gpu_evidence.sh TAG
 set -o pipefail
@@ -17,9 +18,9 @@ F=$(find $O/pmc_FETCH_SIZE -name "*counter_collection.csv" | head -1)
 W=$(find $O/pmc_WRITE_SIZE -name "*counter_collection.csv" | head -1)
 python tools/traffic_from_pmc.py $F $W profiles/traffic_c3.json "bench.py (C3), lease $TAG" || exit 3
 cp profiles/traffic_c3.json $O/traffic_c3.json
-timeout -k 10 500 python bench.py > $O/bench_c3.json 2> $O/bench_c3.err || { echo "bench failed"; tail -5 $O/bench_c3.err; exit 3; }
+timeout -k 10 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_c3.json 2> $O/bench_c3.err || { echo "bench failed"; tail -5 $O/bench_c3.err; exit 3; }
 python -c "import json;d=json.load(open('$O/bench_c3.json'));r=d['roofline'];print('C3', round(d['value']), 'ms', round(d['ms_per_step'],1), 'frac', round(r['frac'],3), 'traffic', r['traffic'], 'k_persist ms', round(r['ms_per_launch'],1), 'cpu', round(d['cpu_baseline']['value']))"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python bench.py --no-cpu --no-e2e > $O/prof.log 2>&1 || { echo "prof failed"; exit 3; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --no-e2e > $O/prof.log 2>&1 || { echo "prof failed"; exit 3; }
 find $O/prof -name "*kernel_stats.csv" | head -1 | xargs -r cut -d, -f1-4 | grep -E "Name|k_persist"
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
 P2="SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_SALU"

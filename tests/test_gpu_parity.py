@@ -372,6 +372,43 @@ def test_team_sizes_match_reference(sgpmod, name, teams):
         np.testing.assert_allclose(out["discr"][0, :it + 1], fx["discr"], rtol=1e-7)
 
 
+@pytest.mark.parametrize("T", [64, 65, 100, 255])
+def test_c4_group_leader_team_sizes(sgpmod, T):
+    """C4's field (2048^2, cooperative plan) at explicit team sizes around
+    the flag-barrier cutover: 64 members take the flat flag
+    barriers, 65 / 100 / 255 the eight group leaders with uneven groups
+    (T % 8 = 1, 4, 7; 255 also polls wide reductions, BSGP_RED_POLL_MAX).
+    The team size used is reported, no barrier timed out, and the discrepancy
+    of the reference's own C4 run (make_golden.py c4) is met at every one of
+    three iterations."""
+    import cpu_bench
+    fx = golden("ref_c4_maxit20.npz")
+    gn, psf = cpu_bench.make_stamp(0, 2048, 64, 5000, circular=True)
+    kw = ref_kwargs(fx)
+    b = kw.pop("betaParam")
+    kw["MAXIT"] = 3
+    out = sgpmod.sgp_betaDiv_batch(gn[None], psf, 100.0, betaParams=b, team=T, **kw)
+    assert out["counters"][0, 5] == T
+    assert out["counters"][0, 3] & 4 == 0
+    assert int(out["iters"][0]) == 3
+    np.testing.assert_allclose(out["discr"][0, :4], fx["discr"][:4], rtol=1e-7)
+    assert abs(out["x"][0].sum() / np.sum(gn - 100.0) - 1) < 1e-8
+
+
+def test_team_size_clamped_to_barrier_words(sgpmod):
+    """A team request above kMaxTeam (512, the barrier words and the group
+    leaders' polls of bsgp_device.hpp) is clamped, never run."""
+    import cpu_bench
+    fx = golden("ref_c4_maxit20.npz")
+    gn, psf = cpu_bench.make_stamp(0, 2048, 64, 5000, circular=True)
+    kw = ref_kwargs(fx)
+    b = kw.pop("betaParam")
+    kw["MAXIT"] = 1
+    out = sgpmod.sgp_betaDiv_batch(gn[None], psf, 100.0, betaParams=b, team=4096, **kw)
+    assert 1 <= out["counters"][0, 5] <= 512
+    assert out["counters"][0, 3] & 4 == 0
+
+
 def test_auto_team_spreads_small_batches(sgpmod):
     """team=0 (default): a single image uses many workgroups, a batch as large
     as the CU count uses one each."""
