@@ -31,11 +31,13 @@ def _run(args, timeout=240):
 @pytest.mark.gpu
 def test_bench_two_ranks_weak_c3_on_one_gpu():
     """C3 at 64 images per rank, MAXIT 5 (stop rule 1: every image runs 5
-    iterations): n_gpus 2, images_total = 2 x per-rank, the summed
-    image-iterations of both ranks' real solves, value = that / max wall."""
+    iterations), one workgroup per image as C3 runs (the persistent solver;
+    two ranks' spinning teams on one device are not what a node runs): n_gpus
+    2, images_total = 2 x per-rank, the summed image-iterations of both
+    ranks' real solves, value = that / max wall."""
     B, M = 64, 5
     r = _run(["--gpus", "2", "--steps", "2", "--warmup", "1", "--maxit", str(M), "--batch", str(B),
-              "--no-cpu", "--no-e2e", "--no-profile"])
+              "--team", "1", "--no-cpu", "--no-e2e", "--no-profile"])
     assert r["n_gpus"] == 2 and r["scaling"] == "weak"
     c = r["config"]
     assert c["images_per_gpu"] == B and c["images_total"] == 2 * B

@@ -544,8 +544,14 @@ def test_profiled_solve_reports_every_kernel_class(sgpmod):
     assert np.all(b["kernel_ms"][:5] > 0)
     c = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, team=1, profile=True, persistent=1, **kw)
     np.testing.assert_array_equal(a["x"], c["x"])
-    assert list(c["launches"]) == [1, 0, 0, 0, 0, 1]  # setup, then every iteration in one launch
-    assert c["kernel_ms"][5] > 0
+    # every setup and every iteration in one launch (the setups folded into
+    # k_persist, DESIGN §3.4: no k_setup launch)
+    assert list(c["launches"]) == [0, 0, 0, 0, 0, 1]
+    assert c["kernel_ms"][0] == 0 and c["kernel_ms"][5] > 0
+    # stop rule 3 keeps the ready ring, whose setups stay a k_setup launch
+    d = sgpmod.sgp_betaDiv_batch(gns, fx["psf"], 100.0, team=1, profile=True, persistent=1,
+                                 **dict(kw, stop_criterion=3, tol_convergence=1e-9))
+    assert list(d["launches"]) == [1, 0, 0, 0, 0, 1]
 
 
 # ------------------------------------------------------- float32 storage (C4)
