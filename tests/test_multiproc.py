@@ -104,3 +104,25 @@ def test_bench_fails_fast_when_a_rank_dies(fail_rank):
     assert el < 30, el
     assert f"rank {fail_rank} exited with 1" in out.stderr
     assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
+
+
+def test_kernel_bytes_model_c3():
+    """bench.py's algorithmic byte model on C3's shape with the
+    device's per-iteration counters of a 100-iteration solve: the per-kernel
+    formulas, the setup's 140 B/px + 12 S + 3 TF per image, and the total the
+    roofline divides by (1.65 TB with the setups, 1.636 TB without)."""
+    import numpy as np
+    import bench
+    B, it, N = 1024, 100, 256 * 256
+    cnt = np.zeros((B, 8))
+    cnt[:, 2] = 1.407578125 * it          # line-search passes (BENCH_r05 counters)
+    cnt[:, 6] = 1.698193359375 * it       # projection full passes
+    cnt[:, 7] = 0.15436440110206603 * it * N  # list entries read
+    b = bench.kernel_bytes(256, 256, 270, 136, cnt, np.full(B, it), beta=True, series=True,
+                           compact=True, bmap=False, fused_at_col=True)
+    S, TF = 16.0 * 256 * 136, 16.0 * 270 * 136
+    assert b["k_setup"] == B * (140.0 * N + 12 * S + 3 * TF)
+    assert b["k_col"] == B * it * (2 * S + TF)
+    iters_bytes = sum(v for k, v in b.items() if k != "k_setup")
+    assert abs(iters_bytes / 1.6356e12 - 1) < 2e-3   # the round-5 driver line's bytes
+    assert abs(b["k_setup"] / iters_bytes - 0.011) < 0.002
