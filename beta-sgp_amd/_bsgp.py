@@ -251,16 +251,27 @@ class Plan:
                 raise BsgpError(
                     f"save=True keeps {params.MAXIT} iterates of {self.H}x{self.W} on the device "
                     f"({need / 2**30:.1f} GiB, {free / 2**30:.1f} GiB free): lower MAXIT")
+        # the small outputs are views of two zeroed blocks (two fill launches
+        # instead of eight on the latency-bound single-image calls)
+        nd = B * M1 * (2 + bool(want_times) + (obj is not None)) + B
+        d64 = torch.zeros(nd, **f64)
+        i32 = torch.zeros(B * (M1 + 1) + 2 * 8 * B, dtype=torch.int32, device=dev)
+        parts = iter(torch.split(d64, [B * M1] * (2 + bool(want_times) + (obj is not None)) + [B]))
+        discr, crit = next(parts).view(B, M1), next(parts).view(B, M1)
+        times = next(parts).view(B, M1) if want_times else None
+        err = next(parts).view(B, M1) if obj is not None else None
+        beta_final = next(parts)
+        cnt, iters, flags = torch.split(i32, [2 * 8 * B, B, B * M1])  # (int64 counters first: aligned)
         out = {
             "x": torch.empty_like(gn),
-            "iters": torch.zeros(B, dtype=torch.int32, device=dev),
-            "discr": torch.zeros(B, M1, **f64),
-            "times": torch.zeros(B, M1, **f64) if want_times else None,
-            "crit": torch.zeros(B, M1, **f64),
-            "flags": torch.zeros(B, M1, dtype=torch.int32, device=dev),
-            "beta_final": torch.zeros(B, **f64),
-            "counters": torch.zeros(B, 8, dtype=torch.int64, device=dev),
-            "err": torch.zeros(B, M1, **f64) if obj is not None else None,
+            "iters": iters,
+            "discr": discr,
+            "times": times,
+            "crit": crit,
+            "flags": flags.view(B, M1),
+            "beta_final": beta_final,
+            "counters": cnt.view(torch.int64).view(B, 8),
+            "err": err,
             "x_iter": (torch.zeros(B, params.MAXIT, self.H, self.W, **f64) if want_iterates
                        else None),
         }
@@ -470,6 +481,29 @@ def to_dev(a):
     if not a.flags.writeable:
         a = a.copy()
     return torch.from_numpy(a).to("cuda")
+
+
+def to_dev_async(a):
+    """Host array -> float64 device tensor through page-locked memory (torch's
+    caching host allocator, which does not hand the block out again before
+    the copy has run), enqueued on the current stream without waiting: the
+    single-image drop-in's inputs (a pageable copy stages through the
+    runtime's own buffer and blocks)."""
+    a = np.asarray(a, dtype="<f8")
+    h = torch.empty(a.shape, dtype=torch.float64, pin_memory=True)
+    h.numpy()[...] = a
+    return h.to("cuda", non_blocking=True)
+
+
+def to_host(tensors):
+    """Device tensors (dict; None entries kept) -> numpy arrays: every copy
+    enqueued on the current stream into page-locked memory, ONE stream
+    synchronisation, then plain numpy copies (nothing page-locked escapes to
+    the caller)."""
+    pinned = {k: (None if t is None else t.to("cpu", non_blocking=True))
+              for k, t in tensors.items()}
+    torch.cuda.current_stream().synchronize()
+    return {k: (None if t is None else t.numpy().copy()) for k, t in pinned.items()}
 
 
 def project_df_dev(b, c, dia, scaling, ccd_sat_level, lambda_, dlambda_, tol_lam, biter, siter,

@@ -229,28 +229,61 @@ def _params(variant, init_recon, proj_type, stop_criterion, MAXIT, gamma, beta, 
     return p
 
 
-def _write_log(stop_criterion, verbose, discr, crit, flags, MAXIT, tol):
-    """The reference's sgp.log lines (sgp.py:291-298, 351-352, 399-411)."""
-    log = logging.getLogger()
-    n = len(discr)
+def _log_records(stop_criterion, verbose, discr, crit, flags, MAXIT, tol):
+    """The reference's sgp.log records (sgp.py:291-298, 351-352, 399-411), in
+    order, as (level, message)."""
+    I, W = logging.INFO, logging.WARNING
+    recs = []
     if verbose:
         if stop_criterion == 2:
-            log.info('it 0 || x_k - x_(k-1) ||^2 / || x_k ||^2 0 \n')
+            recs.append((I, 'it 0 || x_k - x_(k-1) ||^2 / || x_k ||^2 0 \n'))
         elif stop_criterion == 3:
-            log.info('it 0 | f_k - f_(k-1) | / | f_k | 0 \n')
+            recs.append((I, 'it 0 | f_k - f_(k-1) | / | f_k | 0 \n'))
         elif stop_criterion == 4:
-            log.info(f'it 0 D_k {discr[0]} \n')
-    for k in range(1, n):
+            recs.append((I, f'it 0 D_k {discr[0]} \n'))
+    for k in range(1, len(discr)):
         if verbose and flags[k] & 1:
-            log.warning("\tWarning, fv >= fr")
+            recs.append((W, "\tWarning, fv >= fr"))
         if stop_criterion == 1:
-            log.info(f'it {k} of  {MAXIT}\n')
+            recs.append((I, f'it {k} of  {MAXIT}\n'))
         elif stop_criterion == 2:
-            log.info(f'it {k} || x_k - x_(k-1) ||^2 / || x_k ||^2 {crit[k]} tol {tol}\n')
+            recs.append((I, f'it {k} || x_k - x_(k-1) ||^2 / || x_k ||^2 {crit[k]} tol {tol}\n'))
         elif stop_criterion == 3:
-            log.info(f'it {k} | f_k - f_(k-1) | / | f_k | {crit[k]} tol {tol}\n')
+            recs.append((I, f'it {k} | f_k - f_(k-1) | / | f_k | {crit[k]} tol {tol}\n'))
         elif stop_criterion == 4:
-            log.info(f'it {k} D_k {discr[k]} tol {tol}\n')
+            recs.append((I, f'it {k} D_k {discr[k]} tol {tol}\n'))
+    return recs
+
+
+def _write_log(stop_criterion, verbose, discr, crit, flags, MAXIT, tol):
+    """The reference's sgp.log lines.  With the logging set-up the reference
+    itself makes (sgp.py:104 / :564: basicConfig(filename='sgp.log'), one
+    FileHandler, the default format, nothing filtered) the lines go to the
+    file in ONE write, byte for byte what one logging call per line writes
+    (~20 us per record through the logging machinery: 0.7 ms of a 32-iteration
+    call of the application's); any other set-up gets one logging call per
+    record."""
+    recs = _log_records(stop_criterion, verbose, discr, crit, flags, MAXIT, tol)
+    log = logging.getLogger()
+    hs = log.handlers
+    h = hs[0] if len(hs) == 1 else None
+    fast = (h is not None and type(h) is logging.FileHandler and not h.filters
+            and not log.filters and h.formatter is not None
+            and h.formatter._fmt == logging.BASIC_FORMAT and h.level <= logging.INFO
+            and log.isEnabledFor(logging.INFO) and not logging.root.manager.disable
+            and h.stream is not None)
+    if not fast:
+        for lvl, msg in recs:
+            log.log(lvl, msg)
+        return
+    text = "".join(f"{logging.getLevelName(lvl)}:{log.name}:{msg}{h.terminator}"
+                   for lvl, msg in recs)
+    h.acquire()
+    try:
+        h.stream.write(text)
+        h.flush()
+    finally:
+        h.release()
 
 
 SAVE_DIR = "SGP_reconstructed_images/"
@@ -360,11 +393,14 @@ def _run(variant, gn, psf, bkg, init_recon, proj_type, stop_criterion, MAXIT, ga
             np.random.seed(42)
             x0 = np.random.randn(*gn.shape)
     _B.require_gpu()  # the product path runs on the device or not at all
-    gd = _B.to_dev(np.asarray(g, dtype=np.float64).reshape(1, *_shape))
-    bd = _B.to_dev(np.asarray(bk, dtype=np.float64).reshape((1, *_shape) if bkg_is_map else (1,)))
-    fd = None if fl is None else _B.to_dev(fl)
-    xd = None if x0 is None else _B.to_dev(np.asarray(x0, dtype=np.float64).reshape(1, *_shape))
-    od = None if not errflag else _B.to_dev(np.asarray(obj, dtype=np.float64).reshape(1, *_shape))
+    # inputs through page-locked memory, enqueued without waiting (_B.to_dev_async)
+    gd = _B.to_dev_async(np.asarray(g, dtype=np.float64).reshape(1, *_shape))
+    bd = _B.to_dev_async(np.asarray(bk, dtype=np.float64).reshape((1, *_shape) if bkg_is_map
+                                                                  else (1,)))
+    fd = None if fl is None else _B.to_dev_async(fl)
+    xd = None if x0 is None else _B.to_dev_async(np.asarray(x0, dtype=np.float64).reshape(1, *_shape))
+    od = None if not errflag else _B.to_dev_async(np.asarray(obj, dtype=np.float64).reshape(1,
+                                                                                           *_shape))
     gs = None
     if save:
         g_f = g
@@ -379,10 +415,13 @@ def _run(variant, gn, psf, bkg, init_recon, proj_type, stop_criterion, MAXIT, ga
         gd, bd, xd, od = (None if t is None else t.expand(nb, *t.shape[1:]).contiguous()
                           for t in (gd, bd, xd, od))
         fd = None if fd is None else fd.expand(nb).contiguous()
-        b0 = _B.to_dev(np.asarray(betas, dtype=np.float64))
+        b0 = _B.to_dev_async(np.asarray(betas, dtype=np.float64))
     with _B.lease_plan(_shape[0], _shape[1], psf, mode) as plan:
-        out = plan.solve(gd, bd, prm, flux=fd, x0=xd, obj=od, beta0=b0, want_iterates=bool(save))
-    _B.torch.cuda.current_stream().synchronize()
+        dout = plan.solve(gd, bd, prm, flux=fd, x0=xd, obj=od, beta0=b0, want_iterates=bool(save))
+    # every output the caller gets, in one round of copies and one stream sync
+    # (each .cpu() had waited for the stream on its own)
+    out = _B.to_host({k: dout[k] for k in ("x", "iters", "discr", "times", "crit", "flags",
+                                           "beta_final", "counters", "err")})
     _B.check_status(out["counters"])
     def log_run(i, discr):
         if verbose or stop_criterion in (1, 2, 3, 4):
@@ -391,30 +430,30 @@ def _run(variant, gn, psf, bkg, init_recon, proj_type, stop_criterion, MAXIT, ga
                 tol = 1 + 1 / float(np.mean(gn if f32 else np.asarray(gn, dtype=np.float64)))
             if stop_criterion == 2 and verbose:
                 tol = tol * tol
-            _write_log(stop_criterion, verbose, discr, out["crit"][i].cpu().numpy(),
-                       out["flags"][i].cpu().numpy(), MAXIT, tol)
+            _write_log(stop_criterion, verbose, discr, out["crit"][i],
+                       out["flags"][i], MAXIT, tol)
 
     if betas is not None:
         res = []
         for i in range(len(betas)):
             it = int(out["iters"][i])
-            discr = out["discr"][i, :it + 1].cpu().numpy()
+            discr = out["discr"][i, :it + 1]
             log_run(i, discr)  # each candidate is one sgp_betaDiv call in the application
-            res.append((out["x"][i].cpu().numpy().reshape(_shape), it, discr,
-                        out["times"][i, :it + 1].cpu().numpy(),
+            res.append((out["x"][i].reshape(_shape), it, discr,
+                        out["times"][i, :it + 1],
                         {"beta": float(out["beta_final"][i]),
-                         "counters": out["counters"][i].cpu().numpy(), "err": None,
+                         "counters": out["counters"][i], "err": None,
                          "log": lambda i=i, d=discr: log_run(i, d)}))
         return res
     it = int(out["iters"][0])
-    discr = out["discr"][0, :it + 1].cpu().numpy()
-    times = out["times"][0, :it + 1].cpu().numpy()
+    discr = out["discr"][0, :it + 1]
+    times = out["times"][0, :it + 1]
     log_run(0, discr)
     if save:
-        _save_iterates(out["x_iter"][0, :it].cpu().numpy(), gs, _shape)
-    x = out["x"][0].cpu().numpy().reshape(_shape)
-    extra = {"beta": float(out["beta_final"][0]), "counters": out["counters"][0].cpu().numpy(),
-             "err": _err_layout(out["err"][0].cpu().numpy(), it) if errflag else None}
+        _save_iterates(dout["x_iter"][0, :it].cpu().numpy(), gs, _shape)  # (can be large)
+    x = out["x"][0].reshape(_shape)
+    extra = {"beta": float(out["beta_final"][0]), "counters": out["counters"][0],
+             "err": _err_layout(out["err"][0], it) if errflag else None}
     return x, it, discr, times, extra
 
 
