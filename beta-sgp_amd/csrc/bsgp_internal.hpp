@@ -19,6 +19,10 @@ struct ImgState {
   int64_t proj_passes, proj_list;  // projection passes over the image / list entries read
   double sc, flux, bks_scalar, lo, hi, Dcoeff, tol, t0;
   double fv, alpha, tau, lr, init_lr, beta, lam_p, gd, lam;
+  // projection history for the first pass's split bracket (cached_projection):
+  // the last multiplier over the step length it was found at, and the last
+  // search's first secant point over its root (0: none yet)
+  double lam_ratio, kappa;
   double konst;  // lambda-independent objective sum at `beta` (sum s*gn^b / sum gn)
   // compact observed image (params.gn_compact): 0 = gn_s stored in f64; 1 = the
   // raw counts stored in f32, gn_s = raw (scale_data 0/2); 2 = gn_s = raw / sc.
