@@ -51,6 +51,13 @@ namespace bsgp {
 #ifndef BSGP_LS_ATTR
 #define BSGP_LS_ATTR __attribute__((amdgpu_waves_per_eu(COOP ? 1 : ((K <= 2 && !ADAPT) ? 3 : 2))))
 #endif
+// line search: pass 1 also sums the second trial (lam = beta) directly.  On in
+// the per-wave persistent build only (bsgp_persist.hip; A/B same box: C3 +0.5 %,
+// 1.41 -> 1.21 passes per iteration, C5 -0.1 %); the cooperative k_ls spills
+// with it (C4 -3.7 %, C2 -0.7 %).
+#ifndef BSGP_LS1_K2
+#define BSGP_LS1_K2 0
+#endif
 #ifndef BSGP_SERIES_BOUND
 #define BSGP_SERIES_BOUND 1  // closed-form trials past lam*max|u| <= 0.01 under the tail bound
 #endif
@@ -1204,9 +1211,20 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
   // binom(b-1, m)), not in VGPRs across the trial passes
   double* ser = red + kWaves * kMaxRed + kMaxRed + 8;
   double rho = INFINITY;
+  // Pass 1 also sums the second trial (lam = beta) directly when the series is
+  // on: where max|u| keeps that trial out of the closed form (the iterations
+  // whose first trial fails at a large step), it is taken from these sums
+  // instead of a direct pass over the image.  Both sums come from the same
+  // per-pixel arithmetic as a direct pass's (x0 + lam d_tf), summed in the
+  // pass's own order.
+  const bool k2 = BSGP_LS1_K2 && series;
+  const double lam2 = lam * P.beta;
+  double f2 = NAN;     // the second trial's objective from pass 1
+  bool have2 = false;  // f2 holds the next trial's objective
   // ---- pass 1, fused into the inverse rows that produce d_tf: lam = 1 direct
   {
-    constexpr int N1 = 4 + 2 * (MS + 1);  // lam=1 sums, const, dDiv/dbeta, P_m, Q_m
+    constexpr int O2 = 4 + 2 * (MS + 1);
+    constexpr int N1 = O2 + (BSGP_LS1_K2 ? 2 : 0);  // lam=1 sums, const, dDiv/dbeta, P_m, Q_m, lam=beta sums
     double t1[N1];
 #pragma unroll
     for (int k = 0; k < N1; ++k) t1[k] = 0.0;
@@ -1252,6 +1270,12 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
         }
         const double au = fabs(u);
         umax = (au > umax || au != au || !(a > 0)) ? (a > 0 ? au : INFINITY) : umax;
+        if constexpr (BSGP_LS1_K2) {
+          if (k2) {
+            const double x2 = x0 + lam2 * v;
+            obj.template terms_m<MODE>(x2, x2 + bkv, g, &t1[O2]);
+          }
+        }
       }
     });
     // sums and max|u| in one team barrier (the same bits as team_sum + team_max)
@@ -1280,6 +1304,12 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
       if (adapt) {  // sgp.py:798-800: beta -= lr * mean(dDiv/dbeta)
         const double bgrad = (obj.beta == 0.0 || obj.beta == 1.0) ? 0.0 : t1[3] / N;
         obj.set_beta(obj.beta - lr_st * bgrad);
+      }
+      if constexpr (BSGP_LS1_K2) {
+        if (k2) {
+          f2 = obj.combine(konst, t1[O2], t1[O2 + 1], flux, (double)N);
+          have2 = true;
+        }
       }
     }
   }
@@ -1316,6 +1346,24 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
   };
   PH_T(tk1);
   while (!accepted) {
+    if (have2 && !series_ok(lam)) {
+      // the second trial, summed by pass 1 (f2 is NaN only if its sums are:
+      // then it fails the test, as a direct pass's NaN would)
+      have2 = false;
+      ++nls;
+      if (f2 <= fr + P.gamma * lam * gd || lam < 1e-12) {
+        f_acc = f2;
+        accepted = true;
+        break;
+      }
+      lam = lam * P.beta;
+      if (nls > ls_cap) {
+        status = 1;
+        break;
+      }
+      continue;
+    }
+    have2 = false;
     if (series && series_ok(lam)) {
       // closed-form trial: no pass over the image
       double s0 = 0.0, s1 = 0.0, lm = 1.0;

@@ -9,6 +9,9 @@
 
 #include <vector>
 
+#ifndef BSGP_LS1_K2
+#define BSGP_LS1_K2 1  // (bsgp_kernels.hpp)
+#endif
 #include "bsgp_kernels.hpp"
 
 namespace bsgp {
