@@ -52,9 +52,10 @@ namespace bsgp {
 #define BSGP_LS_ATTR __attribute__((amdgpu_waves_per_eu(COOP ? 1 : ((K <= 2 && !ADAPT) ? 3 : 2))))
 #endif
 // line search: pass 1 also sums the second trial (lam = beta) directly.  On in
-// the per-wave persistent build only (bsgp_persist.hip; A/B same box: C3 +0.5 %,
-// 1.41 -> 1.21 passes per iteration, C5 -0.1 %); the cooperative k_ls spills
-// with it (C4 -3.7 %, C2 -0.7 %).
+// the per-wave float64 builds (bsgp_persist.hip and bsgp_solver.hip's phase
+// kernels, which must stay bitwise equal to it; A/B same box: C3 +0.5 %,
+// 1.41 -> 1.21 passes per iteration, C5 -0.1 %); never in the cooperative
+// kernels, whose k_ls spills with it (C4 -3.7 %).
 #ifndef BSGP_LS1_K2
 #define BSGP_LS1_K2 0
 #endif
@@ -1217,14 +1218,14 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
   // instead of a direct pass over the image.  Both sums come from the same
   // per-pixel arithmetic as a direct pass's (x0 + lam d_tf), summed in the
   // pass's own order.
-  const bool k2 = BSGP_LS1_K2 && series;
+  const bool k2 = BSGP_LS1_K2 && !COOP && series;
   const double lam2 = lam * P.beta;
   double f2 = NAN;     // the second trial's objective from pass 1
   bool have2 = false;  // f2 holds the next trial's objective
   // ---- pass 1, fused into the inverse rows that produce d_tf: lam = 1 direct
   {
     constexpr int O2 = 4 + 2 * (MS + 1);
-    constexpr int N1 = O2 + (BSGP_LS1_K2 ? 2 : 0);  // lam=1 sums, const, dDiv/dbeta, P_m, Q_m, lam=beta sums
+    constexpr int N1 = O2 + ((BSGP_LS1_K2 && !COOP) ? 2 : 0);  // lam=1 sums, const, dDiv/dbeta, P_m, Q_m, lam=beta sums
     double t1[N1];
 #pragma unroll
     for (int k = 0; k < N1; ++k) t1[k] = 0.0;
@@ -1270,7 +1271,7 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
         }
         const double au = fabs(u);
         umax = (au > umax || au != au || !(a > 0)) ? (a > 0 ? au : INFINITY) : umax;
-        if constexpr (BSGP_LS1_K2) {
+        if constexpr (BSGP_LS1_K2 && !COOP) {
           if (k2) {
             const double x2 = x0 + lam2 * v;
             obj.template terms_m<MODE>(x2, x2 + bkv, g, &t1[O2]);
@@ -1305,7 +1306,7 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
         const double bgrad = (obj.beta == 0.0 || obj.beta == 1.0) ? 0.0 : t1[3] / N;
         obj.set_beta(obj.beta - lr_st * bgrad);
       }
-      if constexpr (BSGP_LS1_K2) {
+      if constexpr (BSGP_LS1_K2 && !COOP) {
         if (k2) {
           f2 = obj.combine(konst, t1[O2], t1[O2 + 1], flux, (double)N);
           have2 = true;

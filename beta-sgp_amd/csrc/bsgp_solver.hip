@@ -12,6 +12,12 @@
 #include <type_traits>
 #include <vector>
 
+// pass 1 of the line search also sums the second trial (as in the float64
+// persistent build, bsgp_persist.hip: the two stay bitwise equal; the
+// cooperative kernels of this unit keep it off, bsgp_kernels.hpp)
+#ifndef BSGP_LS1_K2
+#define BSGP_LS1_K2 1
+#endif
 #include "bsgp_kernels.hpp"
 
 namespace bsgp {
