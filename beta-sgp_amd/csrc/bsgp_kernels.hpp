@@ -1739,8 +1739,11 @@ static __global__ void k_ring_init(unsigned* queue, int nimg, int img0) {
 #ifndef BSGP_PERSIST_COOP_WAVES
 #define BSGP_PERSIST_COOP_WAVES 2
 #endif
+#ifndef BSGP_PERSIST_WAVES
+#define BSGP_PERSIST_WAVES 3
+#endif
 #define BSGP_PERSIST_ATTR \
-  __attribute__((amdgpu_waves_per_eu(COOP ? BSGP_PERSIST_COOP_WAVES : 3)))
+  __attribute__((amdgpu_waves_per_eu(COOP ? BSGP_PERSIST_COOP_WAVES : BSGP_PERSIST_WAVES)))
 #endif
 
 __device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long long* p) {
