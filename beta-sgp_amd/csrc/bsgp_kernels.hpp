@@ -59,6 +59,12 @@ namespace bsgp {
 #ifndef BSGP_LS1_K2
 #define BSGP_LS1_K2 0
 #endif
+// closed-form line-search trials evaluated kLsLanes at a time, one per lane
+// (ls_phase); 0 = one trial per step (the scalar loop, A/B)
+#ifndef BSGP_LS_SERIES_LANES
+#define BSGP_LS_SERIES_LANES 1
+#endif
+constexpr int kLsLanes = 32;
 #ifndef BSGP_SERIES_BOUND
 #define BSGP_SERIES_BOUND 1  // closed-form trials past lam*max|u| <= 0.01 under the tail bound
 #endif
@@ -1365,6 +1371,58 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
       continue;
     }
     have2 = false;
+    if (BSGP_LS_SERIES_LANES && series && series_ok(lam)) {
+      // Closed-form trials, kLsLanes at once: lane j of every wave evaluates
+      // the j-th next trial, lam * beta^j (the same sequential products the
+      // one-trial-at-a-time loop below forms, so the same bits), with the same
+      // arithmetic as that loop.  The first lane whose trial ends the search
+      // decides: it accepts, it is past the closed form's range (a direct pass
+      // from there on), or it fails at the trial cap.  Every wave computes the
+      // same decision (scalar control stays identical in every thread).
+      constexpr int L = kLsLanes;
+      const int ln = (int)(threadIdx.x & 63u);
+      const int lj = ln < L ? ln : L - 1;
+      double lt = lam;
+      for (int i = 0; i < lj; ++i) lt = lt * P.beta;
+      double s0 = 0.0, s1 = 0.0, lm = 1.0;
+      for (int m = 0; m <= MS; ++m) {
+        s0 += ser[2 * (MS + 1) + m] * lm * ser[m];
+        s1 += ser[3 * (MS + 1) + m] * lm * ser[MS + 1 + m];
+        lm *= lt;
+      }
+      const double fk =
+          obj.combine(konst, obj.c1 * s0, (MODE == 4 ? 1.0 : obj.c2) * s1, flux, (double)N);
+      const bool ok = series_ok(lt);
+      const bool acc = fk <= fr + P.gamma * lt * gd || lt < 1e-12;
+      const bool cap = nls + lj + 1 > ls_cap;
+      const unsigned long long ends = __ballot(ln < L && (!ok || acc || cap));
+      const int j = ends ? __ffsll((long long)ends) - 1 : L - 1;
+      const double lt_j = __shfl(lt, j, 64);
+      const double fk_j = __shfl(fk, j, 64);
+      const bool ok_j = __shfl((int)ok, j, 64) != 0;
+      const bool acc_j = __shfl((int)acc, j, 64) != 0;
+      if (!ok_j) {  // trial j needs a direct pass (its predecessors failed)
+        nls += j;
+        series_evals += j;
+        lam = lt_j;
+        continue;
+      }
+      nls += j + 1;
+      series_evals += j + 1;
+      if (acc_j) {
+        f_acc = fk_j;
+        lam = lt_j;
+        accepted = true;
+        acc_series = true;
+        break;
+      }
+      lam = lt_j * P.beta;
+      if (nls > ls_cap) {
+        status = 1;
+        break;
+      }
+      continue;
+    }
     if (series && series_ok(lam)) {
       // closed-form trial: no pass over the image
       double s0 = 0.0, s1 = 0.0, lm = 1.0;
