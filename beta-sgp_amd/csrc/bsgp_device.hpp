@@ -668,7 +668,7 @@ __device__ __forceinline__ void team_sum(double (&v)[NV], double* red, Team& t) 
 // bounds (max y and -min y).
 template <int NV, int NM>
 __device__ __forceinline__ void team_reduce(double (&v)[NV > 0 ? NV : 1], double (&mx)[NM], double* red,
-                                            Team& t) {
+                                            Team& t, int ph = -1) {
   static_assert(NV + NM <= kMaxRed, "too many values");
   if (t.T == 1) {  // sums first, then maxima: the order of team_sum + team_max
     if constexpr (NV > 0) block_sum<NV>(v, red);
@@ -681,8 +681,14 @@ __device__ __forceinline__ void team_reduce(double (&v)[NV > 0 ? NV : 1], double
     return;
   }
   double* slot = red_slot(t);
+  PH_T(tr0);
   member_partials<NV, NM>(v, mx, red, slot + (size_t)t.m * kMaxRed);
   team_red_barrier(t);
+#ifdef BSGP_PHASE_PROF
+  // (phase profile: the member's own waves, then the other members)
+  const unsigned long long tr1 = __builtin_amdgcn_s_memtime();
+  if (ph >= 0 && threadIdx.x == 0) atomicAdd(&g_phase[ph], tr1 - tr0);
+#endif
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     double s[NV + 1], m[NM];
@@ -728,12 +734,16 @@ __device__ __forceinline__ void team_reduce(double (&v)[NV > 0 ? NV : 1], double
 #pragma unroll
   for (int k = 0; k < NM; ++k) mx[k] = red[kWaves * kMaxRed + NV + k];
   __syncthreads();
+#ifdef BSGP_PHASE_PROF
+  if (ph >= 0 && threadIdx.x == 0) atomicAdd(&g_phase[ph + 1], __builtin_amdgcn_s_memtime() - tr1);
+#endif
   team_red_done(t);
 }
 template <int NV>
-__device__ __forceinline__ void team_sum_max(double (&v)[NV], double& mx, double* red, Team& t) {
+__device__ __forceinline__ void team_sum_max(double (&v)[NV], double& mx, double* red, Team& t,
+                                             int ph = -1) {
   double m[1] = {mx};
-  team_reduce<NV, 1>(v, m, red, t);
+  team_reduce<NV, 1>(v, m, red, t, ph);
   mx = m[0];
 }
 

@@ -1287,7 +1287,7 @@ __device__ __forceinline__ void ls_phase(const SolveArgs& A, int img) {
     });
     // sums and max|u| in one team barrier (the same bits as team_sum + team_max)
     if (series) {
-      team_sum_max<N1>(t1, umax, red, tm);
+      team_sum_max<N1>(t1, umax, red, tm, 25);  // (phase profile slots 25, 26)
       rho = umax;
     } else {
       team_sum<N1>(t1, red, tm);

@@ -28,7 +28,7 @@ SLOTS = {0: "k_dir projection", 1: "k_dir row pass", 2: "k_dir total", 3: "k_col
          16: "  accept rows: operand batches", 17: "  accept rows: FFT", 18: "  accept rows: stores",
          19: "  bb rows: operand batches", 20: "  bb rows: FFT", 21: "  bb rows: stage/unpack",
          22: "  dir rows: operand batches", 23: "  dir rows: FFT", 24: "  dir rows: stores",
-         25: "  coop rows: spectrum gathers", 26: "  coop rows: FFTs", 27: "  coop rows: operands",
+         25: "  coop rows: spectrum gathers | ls1 red.: own waves", 26: "  coop rows: FFTs | ls1 red.: other members", 27: "  coop rows: operands",
          28: "  coop rows: spectrum stores", 29: "  coop cols: loads", 30: "  coop cols: FFT+TF+store",
          31: "persistent: dequeue + wait for the previous iteration"}
 
