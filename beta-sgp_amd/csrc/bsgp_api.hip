@@ -477,23 +477,33 @@ int bsgp_plan_create_checked(int32_t H, int32_t W, const double* psf, int32_t kh
   g.fp.lds_tw = g.fq.lds_tw = -1;
   g.fp.lds_tw2 = g.fq.lds_tw2 = -1;
   g.tw2 = 0;
+  g.twmix = -1;
   // cooperative 2048-point transforms (fft_wide's static plan): their twiddles
   // as a two-level table (bsgp_fft.hpp Tw2, 1.5 KiB) at the start of every
   // kernel's LDS -- the full 32 KiB table does not fit beside the buffers, and
   // from global memory every Stockham stage waited on an L2 round trip
-  if (g.coop && BSGP_COOP_TW2) {
+  // and, after them, the 2048-point column transforms' stage tables
+  // (bsgp_fft.hpp TwMixL: 9 KiB, the global table's entries for the second and
+  // third Stockham stages; loaded by every kernel with the two-level tables)
+  if (g.coop && (BSGP_COOP_TW2 || BSGP_COL_TWMIX)) {
     size_t off = 0;
-    if (g.P == 2048) {
-      g.fp.lds_tw2 = 0;
-      off += (64 + 2048 / 64) * sizeof(cd);
-    }
-    if (g.Q == 2048) {
+    if (BSGP_COOP_TW2) {
       if (g.P == 2048) {
-        g.fq.lds_tw2 = 0;
-      } else {
-        g.fq.lds_tw2 = (int)off;
+        g.fp.lds_tw2 = 0;
         off += (64 + 2048 / 64) * sizeof(cd);
       }
+      if (g.Q == 2048) {
+        if (g.P == 2048) {
+          g.fq.lds_tw2 = 0;
+        } else {
+          g.fq.lds_tw2 = (int)off;
+          off += (64 + 2048 / 64) * sizeof(cd);
+        }
+      }
+    }
+    if (BSGP_COL_TWMIX && !BSGP_COL_TW2 && g.P == 2048) {
+      g.twmix = (int)off;
+      off += (64 + 512) * sizeof(cd);
     }
     g.tw2 = (int)round_up(off, 16);
     p->lds_bytes += g.tw2;

@@ -89,7 +89,9 @@ struct Geo {
   int lpad;      // complex elements per LDS buffer (odd: spreads banks)
   int sld;       // column stride of the stored half spectrum (>= H, even; BSGP_SPEC_PAD)
   int tw2;       // bytes at the start of dynamic LDS holding two-level twiddle tables
-                 // (FftPlan::lds_tw2; cooperative 2048-point plans), else 0
+                 // (FftPlan::lds_tw2; cooperative 2048-point plans) and the column
+                 // transforms' stage tables (twmix), else 0
+  int twmix;     // byte offset of the 2048-point column stage tables (TwMixL), or -1
   FftPlan fp;    // length P (columns)
   FftPlan fq;    // length Q (rows)
   const cd* tfA;   // [Qh][P] transfer function of A, scaled by 1/(P*Q)
@@ -120,6 +122,12 @@ __device__ __forceinline__ void copy_tw2(const FftPlan& f) {
   for (int i = threadIdx.x; i < m; i += blockDim.x) d[i] = f.tw[i < 64 ? i : 64 * (i - 64)];
 }
 __device__ __forceinline__ void load_tw_lds(const Geo& G) {
+  if (G.twmix >= 0) {  // the column transforms' stage tables (TwMixL)
+    extern __shared__ __attribute__((aligned(16))) char bsgp_dyn_lds[];
+    cd* d = reinterpret_cast<cd*>(bsgp_dyn_lds + G.twmix);
+    for (int i = threadIdx.x; i < 64 + 512; i += blockDim.x)
+      d[i] = G.fp.tw[i < 64 ? 32 * i : 4 * (i - 64)];
+  }
   copy_tw(G.fp);
   if (G.fq.lds_tw != G.fp.lds_tw) copy_tw(G.fq);
   copy_tw2(G.fp);
@@ -1050,6 +1058,22 @@ __device__ __forceinline__ void coop_row_inv_fwd_1(const Geo& G, const Part& D, 
 #endif
 // (a template flag, not a modified copy of the plan: a copy of FftPlan lived
 // in scratch memory and every stage of k_col read its fields from there)
+// Column transforms: fft_wide's paths, the 2048-point one reading its
+// second and third stages' twiddles from the LDS stage tables (Geo::twmix,
+// loaded by load_tw_lds; bitwise the global table's values).
+#ifndef BSGP_COL_TWMIX
+#define BSGP_COL_TWMIX 1
+#endif
+// (every cooperative 2048-point plan has the tables: bsgp_plan_create)
+__device__ __forceinline__ cd* col_fft(cd* a, cd* b, const Geo& G, bool inv, int t) {
+  if constexpr (BSGP_COL_TWMIX && !BSGP_COL_TW2) {
+    if (G.fp.n == 2048)
+      return fft_run_static<2048, true, true>(a, b, TwMixL{G.twmix, G.fp.tw}, inv, t, kBlock,
+                                              BlockSync());
+    return fft_run(a, b, G.fp, inv, t, kBlock, BlockSync());
+  }
+  return fft_wide<BSGP_COL_TW2>(a, b, G.fp, inv, t, kBlock, BlockSync());
+}
 __device__ __forceinline__ void coop_col_pair_nyq(const Geo& G, cd* spec, const cd* tf, cd* a,
                                                   cd* b) {
   const int t = threadIdx.x;
@@ -1072,7 +1096,7 @@ __device__ __forceinline__ void coop_col_pair_nyq(const Geo& G, cd* spec, const 
     }
   }
   __syncthreads();
-  cd* Z = fft_wide<BSGP_COL_TW2>(a, b, G.fp, false, t, kBlock, BlockSync());
+  cd* Z = col_fft(a, b, G, false, t);
   cd* o = (Z == a) ? b : a;
   for (int p = t; p < G.P; p += kBlock) {
     cd A, B;
@@ -1081,7 +1105,7 @@ __device__ __forceinline__ void coop_col_pair_nyq(const Geo& G, cd* spec, const 
     o[p] = cmk(X.x - W.y, X.y + W.x);  // X + i W
   }
   __syncthreads();
-  cd* Y = fft_wide<BSGP_COL_TW2>(o, Z, G.fp, true, t, kBlock, BlockSync());
+  cd* Y = col_fft(o, Z, G, true, t);
   for (int p = t; p < G.H; p += kBlock) {
     c0[p] = cmk(Y[p].x, 0.0);
     cN[p] = cmk(Y[p].y, 0.0);
@@ -1118,7 +1142,7 @@ __device__ __forceinline__ void coop_col_conv_1(const Geo& G, const Part& D, cd*
       }
     }
     __syncthreads();
-    cd* Z = fft_wide<BSGP_COL_TW2>(a, b, G.fp, false, t, kBlock, BlockSync());
+    cd* Z = col_fft(a, b, G, false, t);
     for (int p0 = 0; p0 < G.P; p0 += kBlock * kCCH) {
       cd tv[kCCH];
 #pragma unroll
@@ -1130,7 +1154,7 @@ __device__ __forceinline__ void coop_col_conv_1(const Geo& G, const Part& D, cd*
       }
     }
     __syncthreads();
-    cd* Y = fft_wide<BSGP_COL_TW2>(Z, (Z == a) ? b : a, G.fp, true, t, kBlock, BlockSync());
+    cd* Y = col_fft(Z, (Z == a) ? b : a, G, true, t);
     for (int p = t; p < G.H; p += kBlock) col[p] = Y[p];
     __syncthreads();
   }

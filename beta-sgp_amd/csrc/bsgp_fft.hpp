@@ -89,6 +89,11 @@ BSGP_HD cd tw_at(const Tw2& t, int k, bool inv) {
   const cd w = cmul(t.t1[k & 63], t.t2[k >> 6]);
   return inv ? cconj(w) : w;
 }
+template <int STEP, class TW>
+BSGP_HD cd tw_step(const TW& tw, int m, bool inv) {
+  return tw_at(tw, m * STEP, inv);
+}
+
 
 // ---- unrolled butterflies (forward: w = exp(-2 pi i / R); inverse: conj) ----
 BSGP_HD void bfly2(cd* v) {
@@ -409,7 +414,7 @@ BSGP_HD void stage_static(const cd* in, cd* out, TW tw, bool inv, int lane, int 
       for (int r = 0; r < R; ++r) v[r] = in[j + r * nb];
       if constexpr (Ns > 1) {
 #pragma unroll
-        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw_at(tw, r * jm * twstep, inv));
+        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw_step<twstep>(tw, r * jm, inv));
       }
       bfly_r<R>(v, inv);
       const int od = (j / Ns) * Ns * R + jm;
@@ -423,7 +428,7 @@ BSGP_HD void stage_static(const cd* in, cd* out, TW tw, bool inv, int lane, int 
       cd v[R];
       for (int r = 0; r < R; ++r) v[r] = in[j + r * nb];
       if (Ns > 1)
-        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw_at(tw, r * jm * twstep, inv));
+        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw_step<twstep>(tw, r * jm, inv));
       bfly_r<R>(v, inv);
       const int od = (j / Ns) * Ns * R + jm;
       for (int r = 0; r < R; ++r) out[od + r * Ns] = v[r];
@@ -457,6 +462,29 @@ BSGP_HD cd* fft_run_static(cd* a, cd* b, TW tw, bool inv, int lane, int nlanes, 
 #if defined(__HIP_DEVICE_COMPILE__)
 extern __shared__ __attribute__((aligned(16))) char bsgp_dyn_lds[];
 #endif
+
+// Stage tables of the 2048-point radix 8-8-8-4 transform of the cooperative
+// column passes (Geo::twmix): its second stage reads the twiddles w^(32 m)
+// (m < 64), its third w^(4 m) (m < 512), its last w^k.  The first two come
+// from LDS copies of the full table's entries (9 KiB beside the two-level
+// tables), the last from the global table: the same values (bitwise equal to
+// the global table), one global-memory round trip per transform instead of
+// three, and no extra products (the two-level table's product had taken the
+// column kernel past 128 VGPRs).
+struct TwMixL {
+  int off;      // byte offset of the tables in dynamic LDS: [64] w^(32 m), then [512] w^(4 m)
+  const cd* g;  // the global table
+};
+template <int STEP>
+BSGP_HD cd tw_step(const TwMixL& t, int m, bool inv) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const cd* l = reinterpret_cast<const cd*>(bsgp_dyn_lds + t.off);
+  const cd w = STEP == 32 ? l[m] : STEP == 4 ? l[64 + m] : t.g[m * STEP];
+#else
+  const cd w = t.g[m * STEP];
+#endif
+  return inv ? cconj(w) : w;
+}
 
 // Workgroup-wide transform (all kBlock-style lanes, `sync` = workgroup
 // barrier): compile-time radix-8 plan for 2048 (config C4), runtime plan otherwise.
