@@ -8,6 +8,10 @@ set -o pipefail
 TAG=${1:-ev}
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/$TAG; export TMPDIR=/tmp
 O=gpurun_out/$TAG
+# a line under gpurun_out/ every 50 s: C4's CPU-baseline sample prints nothing for
+# minutes, which gpurun's silence watchdog takes for a hang (lease r06f)
+( while sleep 50; do date +%s >> $O/heartbeat.txt; done ) &
+trap "kill $! 2>/dev/null" EXIT
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -5 $O/smoke.log; exit 3; }
 tail -1 $O/smoke.log
 for C in FETCH_SIZE WRITE_SIZE; do
