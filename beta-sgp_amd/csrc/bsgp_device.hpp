@@ -150,27 +150,55 @@ struct WaveSync {
 };
 
 // --------------------------------------------------------------- reductions
+// v of lane (lane ^ O), every lane of the wave active: xor 1 and 2 by DPP
+// quad permutes (VALU, no LDS pipe), xor 4 / 8 / 16 by ds_swizzle's bit mode
+// (no address VGPR), xor 32 by ds_bpermute (__shfl_xor).  The same pairing as
+// __shfl_xor for every O, so the reduction trees below keep their bits.
+#ifndef BSGP_WAVE_DPP
+#define BSGP_WAVE_DPP 1
+#endif
+template <int O>
+__device__ __forceinline__ double xor_lanes(double v) {
+  if constexpr (BSGP_WAVE_DPP && (O == 1 || O == 2)) {
+    constexpr int ctrl = O == 1 ? 0xB1 : 0x4E;  // quad_perm [1,0,3,2] / [2,3,0,1]
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), ctrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), ctrl, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+  } else if constexpr (BSGP_WAVE_DPP && O < 32) {
+    constexpr int pat = (O << 10) | 0x1F;  // bit mode: and 0x1F, or 0, xor O
+    const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), pat);
+    const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), pat);
+    return __hiloint2double(hi, lo);
+  } else {
+    return __shfl_xor(v, O, 64);
+  }
+}
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v += xor_lanes<32>(v);
+  v += xor_lanes<16>(v);
+  v += xor_lanes<8>(v);
+  v += xor_lanes<4>(v);
+  v += xor_lanes<2>(v);
+  v += xor_lanes<1>(v);
   return v;
 }
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    double u = __shfl_xor(v, o, 64);
-    v = (u > v || u != u) ? u : v;  // NaN propagates like np.max
-  }
+template <bool MAX>
+__device__ __forceinline__ double wave_ext_step(double v, double u) {
+  // NaN propagates like np.max / np.min
+  return MAX ? ((u > v || u != u) ? u : v) : ((u < v || u != u) ? u : v);
+}
+template <bool MAX>
+__device__ __forceinline__ double wave_ext(double v) {
+  v = wave_ext_step<MAX>(v, xor_lanes<32>(v));
+  v = wave_ext_step<MAX>(v, xor_lanes<16>(v));
+  v = wave_ext_step<MAX>(v, xor_lanes<8>(v));
+  v = wave_ext_step<MAX>(v, xor_lanes<4>(v));
+  v = wave_ext_step<MAX>(v, xor_lanes<2>(v));
+  v = wave_ext_step<MAX>(v, xor_lanes<1>(v));
   return v;
 }
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    double u = __shfl_xor(v, o, 64);
-    v = (u < v || u != u) ? u : v;
-  }
-  return v;
-}
+__device__ __forceinline__ double wave_max(double v) { return wave_ext<true>(v); }
+__device__ __forceinline__ double wave_min(double v) { return wave_ext<false>(v); }
 
 // Sum NV per-thread values over the workgroup; every thread gets the totals.
 // Wave partials go to LDS, thread i < NV adds the kWaves partials of value i
